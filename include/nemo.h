@@ -1,0 +1,139 @@
+/*
+ * nemo.h -- C-ABI of the MI355X order-score engine for Nested Effects Model
+ * order MCMC (drop-in for the per-step scorer of MrGreyPanda/NEM-MCMC-optimization).
+ *
+ * The reference has no FFI layer: its boundary is the Python method surface of
+ * NEMOrderMCMC.  Each entry point below replaces one of those
+ * methods; the Python host (nemo.nem_order_mcmc) keeps the reference's names
+ * and signatures and delegates here through ctypes.
+ *
+ * Conventions
+ *   - plain pointers and sizes; host buffers are caller-owned and only borrowed
+ *     for the call; device buffers are owned by the context;
+ *   - every call returns NEMO_OK (0) or a negative code, and nemo_last_error()
+ *     (thread-local) explains it; the Python host raises RuntimeError with it;
+ *   - host-pointer calls are synchronous (the context stream is synchronised
+ *     before return); *_dev calls take device pointers and only enqueue work on
+ *     the given stream (hipStream_t passed as void*, NULL = context stream);
+ *   - one context per (device, model); calls on one context must not overlap.
+ *
+ * Layouts (row-major, C order):
+ *   T    [S][S][E]  score table, T[i][j][e]: child i, candidate parent j
+ *   U    [S+1][E]   node LR table, row S = "effect attached to nothing"
+ *   pos  [batch][S] int32 position of every S-gene in the order (inverse of pi)
+ *   w01  [batch][S][S] parent weights already mapped to [0,1]
+ *        (the reference maps with expit inside compute_cell_ratios,
+ *         nem_order_mcmc.py:84-86; methods.py:52-57 passes them unmapped)
+ *   Only entries (i, j) with pos[j] < pos[i] (and, with cap > 0,
+ *   pos[i] - pos[j] <= cap) are read: these are the permissible parents.
+ */
+#ifndef NEMO_H
+#define NEMO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nemo_ctx nemo_ctx;
+
+/* table storage / elementwise arithmetic type */
+enum { NEMO_F64 = 0, NEMO_F32 = 1 };
+
+/* return codes */
+enum {
+  NEMO_OK = 0,
+  NEMO_ERR_ARG = -1,     /* bad argument (shape, pointer, range)          */
+  NEMO_ERR_HIP = -2,     /* HIP runtime error (no device, OOM, launch)    */
+  NEMO_ERR_STATE = -3,   /* tables not staged / capacity not reserved     */
+  NEMO_ERR_OPT = -5      /* a local optimisation did not converge         */
+};
+
+/* per-problem termination codes of the local optimiser (scipy task names) */
+enum {
+  NEMO_LBFGSB_CONV_PGTOL = 0,  /* CONVERGENCE: NORM_OF_PROJECTED_GRADIENT_<=_PGTOL */
+  NEMO_LBFGSB_CONV_REL = 1,    /* CONVERGENCE: REL_REDUCTION_OF_F_<=_FACTR*EPSMCH  */
+  NEMO_LBFGSB_ABNORMAL = 2,    /* ABNORMAL_TERMINATION_IN_LNSRCH                  */
+  NEMO_LBFGSB_MAXITER = 3      /* STOP: TOTAL NO. of ITERATIONS REACHED LIMIT     */
+};
+
+const char* nemo_last_error(void);
+int nemo_version(void);
+/* number of visible HIP devices (0 on a host without GPU; never an error) */
+int nemo_device_count(int* count);
+
+/* ---- context lifetime (replaces NEMOrderMCMC.__init__'s table setup,
+ *      nem_order_mcmc.py:40-46) ------------------------------------------ */
+int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out);
+void nemo_ctx_destroy(nemo_ctx* ctx);
+/* grow per-batch scratch so *_dev calls with up to max_batch evaluations
+ * (and max_chains chains for nemo_optimal_weights_dev) never allocate */
+int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains);
+
+/* ---- A1/A2: stage the model once (nem.py:25-64 outputs) ---------------- */
+int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T);
+
+/* ---- A4+A5: batched order-score evaluation --------------------------------
+ * Replaces NEMOrderMCMC.compute_cell_ratios + calculate_ll
+ * (nem_order_mcmc.py:79-93) and utils.compute_ll (utils.py:84-94).
+ *   ll_out    [batch]           sum_e logsumexp_i cell[i][e]
+ *   cs_out    [batch][E]        per-effect log-sum-exp (nullable)
+ *   cells_out [batch][S+1][E]   cell ratios (nullable)
+ *   ow_out    [batch][S+1][E]   order weights exp(cell - cs) (nullable)
+ * cap = 0: every predecessor is a permissible parent (the reference);
+ * cap > 0: only the `cap` nearest predecessors (build-defined C5 extension). */
+int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, int cap,
+               double* ll_out, double* cs_out, double* cells_out, double* ow_out);
+int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double* d_w01, int cap,
+                   double* d_ll, double* d_cs, double* d_cells, double* d_ow, void* stream);
+
+/* reuse-batched variant: `group` evaluations share every table row read
+ * (group in {1,4,8,16}); same results as nemo_score_dev */
+int nemo_score_group_dev(nemo_ctx* ctx, int batch, int group, const int32_t* d_pos, const double* d_w01,
+                         int cap, double* d_ll, void* stream);
+
+/* ---- utils.compute_ll / calculate_ll on a given cell matrix ------------- */
+int nemo_lse(nemo_ctx* ctx, int rows, const double* cells, double* ll_out, double* cs_out, double* ow_out);
+
+/* ---- A8 core: batch of penalised 1-D local problems -----------------------
+ * Replaces scipy.optimize.minimize(local_ll_sum_penalized, x0,
+ * bounds=[(-inf, inf)], args=(c, x_anc), method='L-BFGS-B', tol=0.01)
+ * (nem_order_mcmc.py:18-23, 167): f(x) = -sum_e log(c_e*expit(x) + 1)
+ *   + |expit(x) - x_anc| + expit(x)*(1 - expit(x)), forward-difference
+ * gradient with absolute step 1e-8, L-BFGS-B 3.0 logic for n = 1.
+ *   c [n][E], anc [n], x0 [n] -> xstar, fstar [n]; nit, nfev, status [n] */
+int nemo_local_opt(nemo_ctx* ctx, int n, const double* c, const double* anc, const double* x0,
+                   double* xstar, double* fstar, int32_t* nit, int32_t* nfev, int32_t* status);
+
+/* ---- A6 fused per-step scorer (get_optimal_weights(init=True, max_iter=1),
+ *      nem_order_mcmc.py:172-208) for a batch of chains --------------------
+ * per chain: eval#1 on w01 (order weights kept on device), the local optimum
+ * of every permissible (i, k) pair (c built from T[i][k], order weights row k,
+ * w01[i][k]; x0 = w01[i][k]; anc[i][k]), then eval#2 on the binarised weights
+ * (sigma(x*) > 0.5 ? sig1 : sig0, sig0 = expit(0), sig1 = expit(1)).
+ *   anc    [nchains][S][S]  clip(inv(I - expit_parent_weights(W)) - I, 0, 1)
+ *   w_new  [nchains][S][S]  expit(x*) at permissible entries (others untouched)
+ *   info   [nchains][S][S]  nullable; status | nit << 4 | nfev << 16 per pair
+ *   ll1, ll_dag [nchains]
+ * Returns NEMO_ERR_OPT (results still written) if any pair ended abnormally. */
+int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
+                         const double* anc, double sig0, double sig1, int cap, double* w_new,
+                         double* ll1, double* ll_dag, int32_t* info);
+int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
+                             const double* d_anc, double sig0, double sig1, int cap, double* d_w_new,
+                             double* d_ll1, double* d_ll_dag, int32_t* d_info, void* stream);
+/* order weights of chain `chain` from the last eval#1 of nemo_optimal_weights:
+ * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
+int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
+
+/* ---- timing of the dominant (score) kernel, for bench.py ---------------- */
+int nemo_timing_enable(nemo_ctx* ctx, int enable);
+/* total milliseconds and number of score-kernel launches since enable/reset */
+int nemo_timing_read(nemo_ctx* ctx, double* total_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEMO_H */

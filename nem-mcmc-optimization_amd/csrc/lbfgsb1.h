@@ -1,0 +1,313 @@
+// lbfgsb1.h -- L-BFGS-B (v3.0 logic, as scipy 1.15 runs it) for ONE unbounded
+// variable, as a wave-uniform device routine.
+//
+// This is the optimiser the reference calls once per permissible (child,
+// parent) pair and MCMC step: scipy.optimize.minimize(..., method='L-BFGS-B',
+// bounds=[(-inf, inf)], tol=0.01) at nem_order_mcmc.py:167.  For n = 1:
+//   * every variable is free, the projected gradient is |g|;
+//   * before the first BFGS update the generalised Cauchy point is
+//     x - g/theta (theta = 1); after it, the compact L-BFGS matrix reduces to
+//     the secant slope y/s of the latest accepted pair, so the subspace step is
+//     -g*s/y;
+//   * lnsrlb: d = z - x (rounded), first trial step 1/|d| at iteration 0 and 1
+//     afterwards, x = z at stp == 1; More-Thuente dcsrch (ftol 1e-3, gtol 0.9,
+//     xtol 0.1, stpmin 0, stpmax 1e10), at most maxls = 20 trials, then restart
+//     (memory dropped) or abnormal termination when no pair is stored;
+//   * stopping: |g| <= pgtol (0.01), (fold - f) <= ftol * max(|fold|,|f|,1),
+//     update skipped when s'y <= eps * (-g0'd * stp).
+// The gradient is scipy's forward difference with absolute step 1e-8
+// (scipy optimize/_numdiff.py): h = 1e-8 unless (x+h)-x == 0, then
+// sqrt(eps)*sign(x)*max(1,|x|); g = (f(x+h) - f(x)) / ((x+h) - x).
+//
+// The objective is supplied by the caller as a functor
+//   void fg(double x, double x1, double& f0, double& f1)
+// that returns f(x) and f(x1) identically in every lane of the wave.
+// Python specification: oracle/lbfgsb1.py (checked against scipy).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace nemo {
+
+struct LbfgsResult {
+  double x, f;
+  int nit, nfev, status;
+};
+
+namespace lb {
+
+constexpr double kEpsMch = 2.220446049250313e-16;
+constexpr double kSqrtEps = 1.4901161193847656e-08;
+constexpr double kStpMax = 1e10;
+constexpr double kFtolLs = 1e-3, kGtolLs = 0.9, kXtolLs = 0.1;
+
+__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+
+// MINPACK-2 dcstep: safeguarded step and interval update.
+__device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy,
+                              double& dy, double& stp, double fp, double dp, bool& brackt,
+                              double stpmin, double stpmax) {
+#pragma clang fp contract(off)
+  const double sgnd = dp * (dx / fabs(dx));
+  double stpf;
+  if (fp > fx) {
+    const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
+    const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
+    const double ts = theta / s;
+    double gamma = s * sqrt(ts * ts - (dx / s) * (dp / s));
+    if (stp < stx) gamma = -gamma;
+    const double p = (gamma - dx) + theta;
+    const double q = ((gamma - dx) + gamma) + dp;
+    const double r = p / q;
+    const double stpc = stx + r * (stp - stx);
+    const double stpq = stx + ((dx / ((fx - fp) / (stp - stx) + dx)) / 2.0) * (stp - stx);
+    stpf = (fabs(stpc - stx) < fabs(stpq - stx)) ? stpc : stpc + (stpq - stpc) / 2.0;
+    brackt = true;
+  } else if (sgnd < 0.0) {
+    const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
+    const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
+    const double ts = theta / s;
+    double gamma = s * sqrt(ts * ts - (dx / s) * (dp / s));
+    if (stp > stx) gamma = -gamma;
+    const double p = (gamma - dp) + theta;
+    const double q = ((gamma - dp) + gamma) + dx;
+    const double r = p / q;
+    const double stpc = stp + r * (stx - stp);
+    const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
+    stpf = (fabs(stpc - stp) > fabs(stpq - stp)) ? stpc : stpq;
+    brackt = true;
+  } else if (fabs(dp) < fabs(dx)) {
+    const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
+    const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
+    const double ts = theta / s;
+    double gamma = s * sqrt(dmax(0.0, ts * ts - (dx / s) * (dp / s)));
+    if (stp > stx) gamma = -gamma;
+    const double p = (gamma - dp) + theta;
+    const double q = (gamma + (dx - dp)) + gamma;
+    const double r = p / q;
+    double stpc;
+    if (r < 0.0 && gamma != 0.0) stpc = stp + r * (stx - stp);
+    else if (stp > stx) stpc = stpmax;
+    else stpc = stpmin;
+    const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
+    if (brackt) {
+      stpf = (fabs(stpc - stp) < fabs(stpq - stp)) ? stpc : stpq;
+      if (stp > stx) stpf = dmin(stp + 0.66 * (sty - stp), stpf);
+      else stpf = dmax(stp + 0.66 * (sty - stp), stpf);
+    } else {
+      stpf = (fabs(stpc - stp) > fabs(stpq - stp)) ? stpc : stpq;
+      stpf = dmin(stpmax, stpf);
+      stpf = dmax(stpmin, stpf);
+    }
+  } else {
+    if (brackt) {
+      const double theta = 3.0 * (fp - fy) / (sty - stp) + dy + dp;
+      const double s = dmax(dmax(fabs(theta), fabs(dy)), fabs(dp));
+      const double ts = theta / s;
+      double gamma = s * sqrt(ts * ts - (dy / s) * (dp / s));
+      if (stp > sty) gamma = -gamma;
+      const double p = (gamma - dp) + theta;
+      const double q = ((gamma - dp) + gamma) + dy;
+      const double r = p / q;
+      stpf = stp + r * (sty - stp);
+    } else if (stp > stx) {
+      stpf = stpmax;
+    } else {
+      stpf = stpmin;
+    }
+  }
+  if (fp > fx) {
+    sty = stp; fy = fp; dy = dp;
+  } else {
+    if (sgnd < 0.0) { sty = stx; fy = fx; dy = dx; }
+    stx = stp; fx = fp; dx = dp;
+  }
+  stp = stpf;
+}
+
+// MINPACK-2 dcsrch as a resumable state machine.
+struct Dcsrch {
+  bool brackt;
+  int stage;
+  double finit, ginit, gtest, width, width1;
+  double stx, fx, gx, sty, fy, gy, stmin, stmax;
+
+  // returns false on ERROR (initial derivative not negative)
+  __device__ __forceinline__ bool start(double stp, double f, double g) {
+#pragma clang fp contract(off)
+    if (!(g < 0.0)) return false;
+    brackt = false;
+    stage = 1;
+    finit = f;
+    ginit = g;
+    gtest = kFtolLs * g;
+    width = kStpMax - 0.0;
+    width1 = width / 0.5;
+    stx = 0.0; fx = f; gx = g;
+    sty = 0.0; fy = f; gy = g;
+    stmin = 0.0;
+    stmax = stp + 4.0 * stp;
+    return true;
+  }
+
+  // one dcsrch call with (f, g) at stp; returns 0 = FG (evaluate new stp),
+  // 1 = CONV, 2 = WARN
+  __device__ __forceinline__ int step(double& stp, double f, double g) {
+#pragma clang fp contract(off)
+    const double stpmin = 0.0, stpmax = kStpMax;
+    const double ftest = finit + stp * gtest;
+    if (stage == 1 && f <= ftest && g >= 0.0) stage = 2;
+    int task = 0;
+    if (brackt && (stp <= stmin || stp >= stmax)) task = 2;
+    if (brackt && stmax - stmin <= kXtolLs * stmax) task = 2;
+    if (stp == stpmax && f <= ftest && g <= gtest) task = 2;
+    if (stp == stpmin && (f > ftest || g >= gtest)) task = 2;
+    if (f <= ftest && fabs(g) <= kGtolLs * (-ginit)) task = 1;
+    if (task != 0) return task;
+    // one dcstep call site on locals (keeps the state in registers): the
+    // modified function psi is used in stage 1 when f fell but not enough
+    const bool modified = stage == 1 && f <= fx && f > ftest;
+    double sx = stx, sy = sty, fxl = fx, gxl = gx, fyl = fy, gyl = gy, fp = f, gp = g;
+    if (modified) {
+      fp = f - stp * gtest;
+      fxl = fx - stx * gtest;
+      fyl = fy - sty * gtest;
+      gp = g - gtest;
+      gxl = gx - gtest;
+      gyl = gy - gtest;
+    }
+    dcstep(sx, fxl, gxl, sy, fyl, gyl, stp, fp, gp, brackt, stmin, stmax);
+    stx = sx;
+    sty = sy;
+    if (modified) {
+      fx = fxl + stx * gtest;
+      fy = fyl + sty * gtest;
+      gx = gxl + gtest;
+      gy = gyl + gtest;
+    } else {
+      fx = fxl; fy = fyl; gx = gxl; gy = gyl;
+    }
+    if (brackt) {
+      if (fabs(sty - stx) >= 0.66 * width1) stp = stx + 0.5 * (sty - stx);
+      width1 = width;
+      width = fabs(sty - stx);
+      stmin = dmin(stx, sty);
+      stmax = dmax(stx, sty);
+    } else {
+      stmin = stp + 1.1 * (stp - stx);
+      stmax = stp + 4.0 * (stp - stx);
+    }
+    stp = dmax(stp, stpmin);
+    stp = dmin(stp, stpmax);
+    if ((brackt && (stp <= stmin || stp >= stmax)) ||
+        (brackt && stmax - stmin <= kXtolLs * stmax))
+      stp = stx;
+    return 0;
+  }
+};
+
+}  // namespace lb
+
+// Minimise a 1-D objective from x0.  `fg(x, x1, f0, f1)` must return the
+// objective at x and at x1 (identical in all lanes).  Written as a state
+// machine with ONE evaluation site so the (large, fully unrolled) objective
+// body is instantiated once.
+template <class FG>
+__device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, double ftol = 0.01, double gtol = 0.01,
+                                        double eps = 1e-8, int maxls = 20, int maxiter = 15000,
+                                        int maxfun = 15000) {
+#pragma clang fp contract(off)
+  using namespace lb;
+  const double tol = (ftol / kEpsMch) * kEpsMch;
+  int nfev = 0, nit = 0, ifun = 0;
+  bool have_pair = false, in_ls = false;
+  double s_last = 0.0, y_last = 0.0, theta = 1.0;
+  double x = x0, f = 0.0, g = 0.0;
+  double z = 0.0, d = 0.0, stp = 0.0, xk = 0.0, fold = 0.0, gold = 0.0, gdold = 0.0;
+  double x_eval = x0;
+  bool have_last = false;
+  double x_last = 0.0, f_last = 0.0, g_last = 0.0;
+  Dcsrch ls;
+  for (;;) {
+    // ---- the single evaluation site: f and forward-difference g at x_eval.
+    // scipy's ScalarFunction memoises the last point: a repeated x costs no
+    // evaluation (and no nfev).
+    if (!(have_last && x_eval == x_last)) {
+      double h = eps;
+      if ((x_eval + h) - x_eval == 0.0)
+        h = kSqrtEps * (x_eval >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(x_eval));
+      const double x1 = x_eval + h;
+      double f0, f1;
+      fg(x_eval, x1, f0, f1);
+      nfev += 2;
+      have_last = true;
+      x_last = x_eval;
+      f_last = f0;
+      g_last = (f1 - f0) / (x1 - x_eval);
+    }
+    x = x_eval;
+    f = f_last;
+    g = g_last;
+
+    if (!in_ls) {
+      if (fabs(g) <= gtol) return LbfgsResult{x, f, 0, nfev, 0};
+    } else {
+      int task = ls.step(stp, f, g * d);
+      if (task == 0) {
+        ++ifun;
+        if (ifun - 1 < maxls) {
+          x_eval = (stp == 1.0) ? z : stp * d + xk;
+          continue;
+        }
+        task = -1;  // iback >= maxls
+      }
+      if (task < 0) {
+        x = xk; f = fold; g = gold;
+        if (!have_pair) return LbfgsResult{x, f, nit, nfev, 2};
+        have_pair = false;
+        theta = 1.0;
+      } else {
+        ++nit;
+        if (fabs(g) <= gtol) return LbfgsResult{x, f, nit, nfev, 0};
+        if ((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))
+          return LbfgsResult{x, f, nit, nfev, 1};
+        if (nit >= maxiter || nfev > maxfun) return LbfgsResult{x, f, nit, nfev, 3};
+        const double gd = g * d;
+        const double r = g - gold;
+        const double rr = r * r;
+        double dr, ddum, s;
+        if (stp == 1.0) { dr = gd - gdold; ddum = -gdold; s = d; }
+        else { dr = (gd - gdold) * stp; s = d * stp; ddum = -gdold * stp; }
+        if (!(dr <= kEpsMch * ddum)) {
+          have_pair = true;
+          s_last = s;
+          y_last = r;
+          theta = rr / dr;
+        }
+      }
+    }
+    // ---- next search direction and line-search start (restarts loop here)
+    for (;;) {
+      if (have_pair) z = x + (-g) * (s_last / y_last);
+      else z = x + (1.0 / theta) * (-g);
+      d = z - x;
+      const double dnorm = sqrt(d * d);
+      stp = (nit == 0) ? dmin(1.0 / dnorm, kStpMax) : 1.0;
+      xk = x; fold = f; gold = g;
+      gdold = g * d;
+      if (gdold < 0.0) {
+        ls.start(stp, f, gdold);
+        ifun = 1;
+        in_ls = true;
+        x_eval = (stp == 1.0) ? z : stp * d + xk;
+        break;
+      }
+      if (!have_pair) return LbfgsResult{x, f, nit, nfev, 2};
+      have_pair = false;
+      theta = 1.0;
+    }
+  }
+}
+
+}  // namespace nemo

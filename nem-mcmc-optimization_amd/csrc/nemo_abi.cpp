@@ -1,0 +1,483 @@
+// nemo_abi.cpp -- the C-ABI (include/nemo.h): context lifetime, staging,
+// argument checking, host<->device transfers and launch sequencing.
+// No arithmetic of the hot path lives here; it is all in nemo_kernels.hip.
+#include "nemo.h"
+#include "nemo_internal.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+using nemo::Ctx;
+
+struct nemo_ctx {
+  Ctx c;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(NEMO_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+  if (*p) {
+    hipFree(*p);
+    *p = nullptr;
+  }
+  if (n == 0) n = 1;
+  return hipMalloc((void**)p, n * sizeof(T));
+}
+
+int check_ctx(nemo_ctx* ctx, bool need_staged) {
+  if (!ctx) return fail(NEMO_ERR_ARG, "null context");
+  if (need_staged && !ctx->c.staged) return fail(NEMO_ERR_STATE, "tables not staged");
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return NEMO_OK;
+}
+
+// every row of pos must be a permutation of 0..S-1
+int check_pos(const int32_t* pos, int batch, int S) {
+  std::vector<char> seen(S);
+  for (int b = 0; b < batch; ++b) {
+    std::fill(seen.begin(), seen.end(), 0);
+    for (int i = 0; i < S; ++i) {
+      const int p = pos[(size_t)b * S + i];
+      if (p < 0 || p >= S || seen[p])
+        return fail(NEMO_ERR_ARG, "pos[%d] is not a permutation of 0..%d", b, S - 1);
+      seen[p] = 1;
+    }
+  }
+  return NEMO_OK;
+}
+
+hipStream_t pick(nemo_ctx* ctx, void* stream) {
+  return stream ? (hipStream_t)stream : ctx->c.stream;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nemo_last_error(void) { return g_err.c_str(); }
+
+int nemo_version(void) { return 10000; }
+
+int nemo_device_count(int* count) {
+  if (!count) return fail(NEMO_ERR_ARG, "null count");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return NEMO_OK;
+}
+
+int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out) {
+  if (!out) return fail(NEMO_ERR_ARG, "null out");
+  *out = nullptr;
+  if (num_s < 2 || num_s > nemo::kMaxS)
+    return fail(NEMO_ERR_ARG, "num_s=%d outside [2, %d]", num_s, nemo::kMaxS);
+  if (num_e < 1) return fail(NEMO_ERR_ARG, "num_e=%d < 1", num_e);
+  if (dtype != NEMO_F64 && dtype != NEMO_F32) return fail(NEMO_ERR_ARG, "dtype=%d", dtype);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(NEMO_ERR_HIP, "no HIP device visible (the engine has no CPU fallback)");
+  if (device < 0 || device >= n) return fail(NEMO_ERR_ARG, "device %d of %d", device, n);
+  HIPCHK(hipSetDevice(device));
+  nemo_ctx* ctx = new nemo_ctx();
+  ctx->c.device = device;
+  ctx->c.S = num_s;
+  ctx->c.E = num_e;
+  ctx->c.dtype = dtype;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return fail(NEMO_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = ctx;
+  return NEMO_OK;
+}
+
+void nemo_ctx_destroy(nemo_ctx* ctx) {
+  if (!ctx) return;
+  Ctx& c = ctx->c;
+  hipSetDevice(c.device);
+  hipStreamSynchronize(c.stream);
+  void* bufs[] = {c.d_eT,   c.d_U,    c.d_pos,  c.d_w01,  c.d_anc,     c.d_rows, c.d_sw,
+                  c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
+                  c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
+  hipStreamDestroy(c.stream);
+  delete ctx;
+}
+
+int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (max_batch < 0 || max_chains < 0) return fail(NEMO_ERR_ARG, "negative capacity");
+  Ctx& c = ctx->c;
+  const size_t S = c.S, E = c.E;
+  const int nb = std::max({max_batch, max_chains, 1});
+  if (nb > c.cap_batch) {
+    HIPCHK(hipStreamSynchronize(c.stream));
+    HIPCHK(dalloc(&c.d_pos, nb * S));
+    HIPCHK(dalloc(&c.d_w01, nb * S * S));
+    HIPCHK(dalloc(&c.d_rows, nb * S * S));
+    HIPCHK(dalloc(&c.d_sw, nb * S * S));
+    HIPCHK(dalloc(&c.d_cnt, nb * S));
+    HIPCHK(dalloc(&c.d_partial, nb * (size_t)c.ntiles()));
+    HIPCHK(dalloc(&c.d_ll, nb));
+    HIPCHK(dalloc(&c.d_cs, nb * E));
+    HIPCHK(dalloc(&c.d_ow, nb * (S + 1) * E));
+    c.cap_batch = nb;
+  }
+  const int nc = std::max(max_chains, 1);
+  if (nc > c.cap_chains) {
+    HIPCHK(hipStreamSynchronize(c.stream));
+    HIPCHK(dalloc(&c.d_anc, nc * S * S));
+    HIPCHK(dalloc(&c.d_pairs, nc * S * S));
+    HIPCHK(dalloc(&c.d_ll2, nc));
+    HIPCHK(dalloc(&c.d_wnew, nc * S * S));
+    HIPCHK(dalloc(&c.d_wdag, nc * S * S));
+    HIPCHK(dalloc(&c.d_info, nc * S * S));
+    c.cap_chains = nc;
+  }
+  return NEMO_OK;
+}
+
+int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!U || !T) return fail(NEMO_ERR_ARG, "null table");
+  Ctx& c = ctx->c;
+  const size_t S = c.S, E = c.E, n = S * S * E;
+  // range of the off-diagonal rows (the ones the score reads)
+  double amax = 0.0;
+  for (size_t i = 0; i < S; ++i)
+    for (size_t j = 0; j < S; ++j) {
+      if (i == j) continue;
+      const double* r = T + (i * S + j) * E;
+      for (size_t e = 0; e < E; ++e) {
+        const double v = r[e];
+        if (!isfinite(v)) return fail(NEMO_ERR_ARG, "T[%zu][%zu][%zu] is not finite", i, j, e);
+        amax = std::max(amax, fabs(v));
+      }
+    }
+  const double lim = c.dtype == NEMO_F64 ? 170.0 : 20.0;
+  if (amax > lim)
+    return fail(NEMO_ERR_ARG, "|T| up to %g exceeds the %s product range (%g)", amax,
+                c.dtype == NEMO_F64 ? "f64" : "f32", lim);
+  for (size_t k = 0; k < (S + 1) * E; ++k)
+    if (isnan(U[k])) return fail(NEMO_ERR_ARG, "U has NaN");
+  HIPCHK(hipStreamSynchronize(c.stream));
+  const size_t esz = c.dtype == NEMO_F64 ? 8 : 4;
+  if (c.d_eT) hipFree(c.d_eT);
+  if (c.d_U) hipFree(c.d_U);
+  c.d_eT = c.d_U = nullptr;
+  HIPCHK(hipMalloc(&c.d_eT, n * esz));
+  HIPCHK(hipMalloc(&c.d_U, (S + 1) * E * esz));
+  double* d_t64 = nullptr;
+  HIPCHK(hipMalloc((void**)&d_t64, n * sizeof(double)));
+  HIPCHK(hipMemcpyAsync(d_t64, T, n * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  HIPCHK(nemo::launch_exp_table(c, d_t64, c.stream));
+  if (c.dtype == NEMO_F64) {
+    HIPCHK(hipMemcpyAsync(c.d_U, U, (S + 1) * E * 8, hipMemcpyHostToDevice, c.stream));
+  } else {
+    std::vector<float> u32((S + 1) * E);
+    for (size_t k = 0; k < u32.size(); ++k) u32[k] = (float)U[k];
+    HIPCHK(hipMemcpyAsync(c.d_U, u32.data(), u32.size() * 4, hipMemcpyHostToDevice, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+  }
+  HIPCHK(hipStreamSynchronize(c.stream));
+  HIPCHK(hipFree(d_t64));
+  c.table_absmax = amax;
+  c.staged = true;
+  return NEMO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// A4+A5
+// ---------------------------------------------------------------------------
+int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double* d_w01, int cap,
+                   double* d_ll, double* d_cs, double* d_cells, double* d_ow, void* stream) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (batch < 0 || cap < 0) return fail(NEMO_ERR_ARG, "batch=%d cap=%d", batch, cap);
+  if (batch == 0) return NEMO_OK;
+  if (batch > c.cap_batch) return fail(NEMO_ERR_STATE, "batch %d > reserved %d", batch, c.cap_batch);
+  if (!d_pos || !d_w01 || !d_ll) return fail(NEMO_ERR_ARG, "null device pointer");
+  hipStream_t st = pick(ctx, stream);
+  HIPCHK(nemo::launch_prep(c, batch, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
+  HIPCHK(nemo::launch_score(c, batch, c.d_rows, c.d_sw, c.d_cnt, d_ll, d_cs, d_cells, d_ow, st));
+  return NEMO_OK;
+}
+
+int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, int cap,
+               double* ll_out, double* cs_out, double* cells_out, double* ow_out) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (batch < 0 || cap < 0) return fail(NEMO_ERR_ARG, "batch=%d cap=%d", batch, cap);
+  if (batch == 0) return NEMO_OK;
+  if (!pos || !w01 || !ll_out) return fail(NEMO_ERR_ARG, "null host pointer");
+  Ctx& c = ctx->c;
+  if ((rc = check_pos(pos, batch, c.S))) return rc;
+  if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
+  const size_t S = c.S, E = c.E;
+  hipStream_t st = c.stream;
+  double* d_cells = nullptr;
+  if (cells_out) HIPCHK(hipMallocAsync((void**)&d_cells, batch * (S + 1) * E * 8, st));
+  HIPCHK(hipMemcpyAsync(c.d_pos, pos, batch * S * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_w01, w01, batch * S * S * 8, hipMemcpyHostToDevice, st));
+  rc = nemo_score_dev(ctx, batch, c.d_pos, c.d_w01, cap, c.d_ll, cs_out ? c.d_cs : nullptr,
+                      d_cells, ow_out ? c.d_ow : nullptr, st);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(ll_out, c.d_ll, batch * 8, hipMemcpyDeviceToHost, st));
+  if (cs_out) HIPCHK(hipMemcpyAsync(cs_out, c.d_cs, batch * E * 8, hipMemcpyDeviceToHost, st));
+  if (ow_out)
+    HIPCHK(hipMemcpyAsync(ow_out, c.d_ow, batch * (S + 1) * E * 8, hipMemcpyDeviceToHost, st));
+  if (cells_out) {
+    HIPCHK(hipMemcpyAsync(cells_out, d_cells, batch * (S + 1) * E * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipFreeAsync(d_cells, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  c.ow_chains = 0;  // d_ow no longer holds fused-step order weights
+  return NEMO_OK;
+}
+
+int nemo_score_group_dev(nemo_ctx* ctx, int batch, int group, const int32_t* d_pos,
+                         const double* d_w01, int cap, double* d_ll, void* stream) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (group != 1 && group != 4 && group != 8 && group != 16)
+    return fail(NEMO_ERR_ARG, "group=%d not in {1,4,8,16}", group);
+  if (group == 1) return nemo_score_dev(ctx, batch, d_pos, d_w01, cap, d_ll, nullptr, nullptr, nullptr, stream);
+  if (batch < 0 || cap < 0) return fail(NEMO_ERR_ARG, "batch=%d cap=%d", batch, cap);
+  if (batch == 0) return NEMO_OK;
+  if (batch > c.cap_batch) return fail(NEMO_ERR_STATE, "batch %d > reserved %d", batch, c.cap_batch);
+  const int ng = (batch + group - 1) / group;
+  const size_t need = (size_t)ng * c.S * c.S * 16;  // sized for the largest group
+  if ((size_t)c.cap_group_batch < need) {
+    // first use only: callers reserve by calling once before timing/capture
+    HIPCHK(hipStreamSynchronize(pick(ctx, stream)));
+    HIPCHK(dalloc(&c.d_grows, (size_t)ng * c.S * c.S));
+    HIPCHK(dalloc(&c.d_gsw, need));
+    HIPCHK(dalloc(&c.d_gcnt, (size_t)ng * c.S));
+    c.cap_group_batch = (int)std::min(need, (size_t)0x7fffffff);
+  }
+  hipStream_t st = pick(ctx, stream);
+  HIPCHK(nemo::launch_prep_group(c, batch, group, cap, d_pos, d_w01, st));
+  HIPCHK(nemo::launch_score_group(c, batch, group, d_ll, st));
+  return NEMO_OK;
+}
+
+int nemo_lse(nemo_ctx* ctx, int rows, const double* cells, double* ll_out, double* cs_out,
+             double* ow_out) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (rows < 1 || !cells || !ll_out) return fail(NEMO_ERR_ARG, "rows=%d / null pointer", rows);
+  if ((rc = nemo_reserve(ctx, 1, 0))) return rc;
+  Ctx& c = ctx->c;
+  const size_t E = c.E;
+  hipStream_t st = c.stream;
+  double *d_cells = nullptr, *d_ow = nullptr;
+  HIPCHK(hipMallocAsync((void**)&d_cells, rows * E * 8, st));
+  if (ow_out) HIPCHK(hipMallocAsync((void**)&d_ow, rows * E * 8, st));
+  HIPCHK(hipMemcpyAsync(d_cells, cells, rows * E * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(nemo::launch_lse(c, rows, d_cells, c.d_ll, cs_out ? c.d_cs : nullptr, d_ow, st));
+  HIPCHK(hipMemcpyAsync(ll_out, c.d_ll, 8, hipMemcpyDeviceToHost, st));
+  if (cs_out) HIPCHK(hipMemcpyAsync(cs_out, c.d_cs, E * 8, hipMemcpyDeviceToHost, st));
+  if (ow_out) HIPCHK(hipMemcpyAsync(ow_out, d_ow, rows * E * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipFreeAsync(d_cells, st));
+  if (d_ow) HIPCHK(hipFreeAsync(d_ow, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return NEMO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// A8 core: generic batch of 1-D problems
+// ---------------------------------------------------------------------------
+int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, const double* x0,
+                   double* xstar, double* fstar, int32_t* nit, int32_t* nfev, int32_t* status) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!cvec || !anc || !x0 || !xstar)))
+    return fail(NEMO_ERR_ARG, "n=%d / null pointer", n);
+  if (n == 0) return NEMO_OK;
+  Ctx& c = ctx->c;
+  if (c.E > 80 * 64) return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by local_opt", c.E);
+  const size_t E = c.E;
+  hipStream_t st = c.stream;
+  double *d_c = nullptr, *d_a = nullptr, *d_x = nullptr, *d_o = nullptr;
+  HIPCHK(hipMallocAsync((void**)&d_c, n * E * 8, st));
+  HIPCHK(hipMallocAsync((void**)&d_a, n * 8, st));
+  HIPCHK(hipMallocAsync((void**)&d_x, n * 8, st));
+  HIPCHK(hipMallocAsync((void**)&d_o, n * 3 * 8, st));
+  HIPCHK(hipMemcpyAsync(d_c, cvec, n * E * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_a, anc, n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_x, x0, n * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(nemo::launch_local_opt_generic(c, n, d_c, d_a, d_x, d_o, st));
+  std::vector<double> o((size_t)n * 3);
+  HIPCHK(hipMemcpyAsync(o.data(), d_o, n * 3 * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipFreeAsync(d_c, st));
+  HIPCHK(hipFreeAsync(d_a, st));
+  HIPCHK(hipFreeAsync(d_x, st));
+  HIPCHK(hipFreeAsync(d_o, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int k = 0; k < n; ++k) {
+    const int32_t info = (int32_t)o[(size_t)k * 3 + 2];
+    xstar[k] = o[(size_t)k * 3];
+    if (fstar) fstar[k] = o[(size_t)k * 3 + 1];
+    if (status) status[k] = info & 15;
+    if (nit) nit[k] = (info >> 4) & 4095;
+    if (nfev) nfev[k] = (info >> 16) & 32767;
+  }
+  return NEMO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// A6 fused per-step scorer
+// ---------------------------------------------------------------------------
+int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
+                             const double* d_anc, double sig0, double sig1, int cap,
+                             double* d_w_new, double* d_ll1, double* d_ll_dag, int32_t* d_info,
+                             void* stream) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (nchains < 0 || cap < 0) return fail(NEMO_ERR_ARG, "nchains=%d cap=%d", nchains, cap);
+  if (nchains == 0) return NEMO_OK;
+  if (nchains > c.cap_chains || nchains > c.cap_batch)
+    return fail(NEMO_ERR_STATE, "nchains %d > reserved %d", nchains, c.cap_chains);
+  if (c.E > 80 * 64) return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by local_opt", c.E);
+  if (!d_pos || !d_w01 || !d_anc || !d_w_new || !d_ll1 || !d_ll_dag)
+    return fail(NEMO_ERR_ARG, "null device pointer");
+  hipStream_t st = pick(ctx, stream);
+  const int npairs = nemo::pairs_per_chain(c.S, cap);
+  // eval #1 with order weights (nem_order_mcmc.py:181-182)
+  HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, c.d_pairs, st));
+  HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll1, nullptr, nullptr, c.d_ow, st));
+  // every permissible pair's local optimum (nem_order_mcmc.py:186-189)
+  HIPCHK(nemo::launch_local_opt_pairs(c, nchains, npairs, c.d_pairs, c.d_rows, d_w01, d_anc, c.d_ow,
+                                      sig0, sig1, d_w_new, c.d_wdag, d_info, st));
+  // eval #2 on the binarised weights (nem_order_mcmc.py:205-207)
+  HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, c.d_wdag, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
+  HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll_dag, nullptr, nullptr, nullptr, st));
+  c.ow_chains = nchains;
+  return NEMO_OK;
+}
+
+int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
+                         const double* anc, double sig0, double sig1, int cap, double* w_new,
+                         double* ll1, double* ll_dag, int32_t* info) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
+  if (nchains == 0) return NEMO_OK;
+  if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  Ctx& c = ctx->c;
+  if ((rc = check_pos(pos, nchains, c.S))) return rc;
+  if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
+  const size_t S = c.S;
+  hipStream_t st = c.stream;
+  HIPCHK(hipMemcpyAsync(c.d_pos, pos, nchains * S * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_w01, w01, nchains * S * S * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_anc, anc, nchains * S * S * 8, hipMemcpyHostToDevice, st));
+  // entries outside the permissible pairs keep the caller's values
+  HIPCHK(hipMemcpyAsync(c.d_wnew, w_new, nchains * S * S * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(c.d_info, 0xff, nchains * S * S * 4, st));
+  rc = nemo_optimal_weights_dev(ctx, nchains, c.d_pos, c.d_w01, c.d_anc, sig0, sig1, cap, c.d_wnew,
+                                c.d_ll, c.d_ll2, c.d_info, st);
+  if (rc) return rc;
+  std::vector<int32_t> inf(nchains * S * S);
+  HIPCHK(hipMemcpyAsync(w_new, c.d_wnew, nchains * S * S * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ll1, c.d_ll, nchains * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ll_dag, c.d_ll2, nchains * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(inf.data(), c.d_info, inf.size() * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (info) memcpy(info, inf.data(), inf.size() * 4);
+  for (size_t k = 0; k < inf.size(); ++k) {
+    if (inf[k] == -1) continue;  // not a permissible pair
+    const int status = inf[k] & 15;
+    if (status >= NEMO_LBFGSB_ABNORMAL) {
+      const size_t b = k / (S * S), i = (k / S) % S, j = k % S;
+      return fail(NEMO_ERR_OPT, "Minimization not successful, Reason: %s (chain %zu, pair %zu<-%zu)",
+                  status == NEMO_LBFGSB_ABNORMAL ? "ABNORMAL_TERMINATION_IN_LNSRCH"
+                                                 : "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT",
+                  b, i, j);
+    }
+  }
+  return NEMO_OK;
+}
+
+int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (chain < 0 || chain >= c.ow_chains || !ow_out)
+    return fail(NEMO_ERR_STATE, "no order weights for chain %d (have %d)", chain, c.ow_chains);
+  const size_t n = (size_t)(c.S + 1) * c.E;
+  HIPCHK(hipMemcpyAsync(ow_out, c.d_ow + (size_t)chain * n, n * 8, hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  return NEMO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// timing
+// ---------------------------------------------------------------------------
+int nemo_timing_enable(nemo_ctx* ctx, int enable) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  HIPCHK(hipStreamSynchronize(c.stream));
+  c.timing = enable != 0;
+  c.ev_used = 0;
+  c.launches = 0;
+  c.timed_ms = 0.0;
+  if (c.timing && c.ev_pool.empty()) {
+    c.ev_pool.resize(8192);
+    for (auto& ev : c.ev_pool) HIPCHK(hipEventCreate(&ev));
+  }
+  return NEMO_OK;
+}
+
+int nemo_timing_read(nemo_ctx* ctx, double* total_ms, int* launches) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  double tot = 0.0;
+  for (size_t k = 0; k + 1 < c.ev_used; k += 2) {
+    HIPCHK(hipEventSynchronize(c.ev_pool[k + 1]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c.ev_pool[k], c.ev_pool[k + 1]));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = c.launches;
+  return NEMO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// nemo_internal.h -- context and launcher declarations shared by the C-ABI
+// (nemo_abi.cpp) and the HIP kernels (nemo_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace nemo {
+
+constexpr int kWave = 64;
+constexpr int kMaxS = 256;         // one prep block covers all S-genes
+constexpr int kScoreWaves = 4;     // waves per score block (child split)
+constexpr int kTileCols = kWave;   // effects per score block
+
+// Device state of one staged model on one GPU.
+struct Ctx {
+  int device = 0;
+  int S = 0, E = 0, dtype = 0;     // dtype: 0 f64, 1 f32
+  hipStream_t stream = nullptr;
+  bool staged = false;
+  double table_absmax = 0.0;       // max |T| over off-diagonal rows
+  void* d_eT = nullptr;            // exp(T) [S][S][E] (dtype)
+  void* d_U = nullptr;             // U [S+1][E] (dtype)
+
+  // per-batch scratch (grown by reserve)
+  int cap_batch = 0, cap_chains = 0;
+  int32_t* d_pos = nullptr;        // [cap][S]
+  double* d_w01 = nullptr;         // [cap][S][S]
+  double* d_anc = nullptr;         // [chains][S][S]
+  int32_t* d_rows = nullptr;       // [cap][S][S]   parent list per child
+  double* d_sw = nullptr;          // [cap][S][S]   weight per list entry
+  int32_t* d_cnt = nullptr;        // [cap][S]
+  int32_t* d_pairs = nullptr;      // [chains][S*S] (child << 16 | list index)
+  double* d_partial = nullptr;     // [cap][ntiles]
+  double* d_ll = nullptr;          // [cap]
+  double* d_ll2 = nullptr;         // [chains]
+  double* d_cs = nullptr;          // [cap][E]
+  double* d_ow = nullptr;          // [max(cap, chains)][S+1][E]
+  double* d_wnew = nullptr;        // [chains][S][S]
+  double* d_wdag = nullptr;        // [chains][S][S]
+  int32_t* d_info = nullptr;       // [chains][S][S]
+  double* d_c = nullptr;           // generic local-opt inputs [n][E] (grown on demand)
+  size_t c_capacity = 0;
+  int ow_chains = 0;               // chains whose order weights d_ow holds
+
+  // grouped (reuse) evaluation scratch
+  int cap_group_batch = 0;
+  int32_t* d_grows = nullptr;
+  double* d_gsw = nullptr;
+  int32_t* d_gcnt = nullptr;
+
+  // timing of the score kernel
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  int launches = 0;
+  double timed_ms = 0.0;
+
+  int ntiles() const { return (E + kTileCols - 1) / kTileCols; }
+};
+
+// ---- launchers (nemo_kernels.hip); all enqueue on `st` and never allocate ----
+// exp() of the staged table (in place conversion from fp64 host layout)
+hipError_t launch_exp_table(Ctx& c, const double* d_T64, hipStream_t st);
+hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                       int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
+                       hipStream_t st);
+hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* d_sw,
+                        const int32_t* d_cnt, double* d_ll, double* d_cs, double* d_cells,
+                        double* d_ow, hipStream_t st);
+hipError_t launch_prep_group(Ctx& c, int batch, int group, int cap, const int32_t* d_pos,
+                             const double* d_w01, hipStream_t st);
+hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStream_t st);
+hipError_t launch_lse(Ctx& c, int rows, const double* d_cells, double* d_ll, double* d_cs,
+                      double* d_ow, hipStream_t st);
+hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
+                                  const int32_t* d_rows, const double* d_w01, const double* d_anc,
+                                  const double* d_ow, double sig0, double sig1, double* d_wnew,
+                                  double* d_wdag, int32_t* d_info, hipStream_t st);
+hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
+                                    const double* d_x0, double* d_out, hipStream_t st);
+
+// number of (child, parent) pairs per chain for a given cap
+int pairs_per_chain(int S, int cap);
+
+}  // namespace nemo

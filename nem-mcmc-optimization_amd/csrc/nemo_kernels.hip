@@ -1,0 +1,667 @@
+// nemo_kernels.hip -- gfx950 kernels of the NEM order-score engine.
+//
+// Hot path:
+//   A4+A5  order score  : cell[i][e] = U[i][e] + sum_{j in pa(i)} log(1 - w_ij + w_ij*exp(T[i][j][e]))
+//                          cs[e] = logsumexp_i cell[i][e];  ll = sum_e cs[e]
+//                          (nem_order_mcmc.py:79-93, utils.py:84-94)
+//   A8     local optimum: one L-BFGS-B 1-D solve per permissible (i, k) pair
+//                          (nem_order_mcmc.py:18-23, 160-170)
+//
+// Layout in HBM (all row-major): eT = exp(T) [S][S][E] in the table dtype,
+// U [S+1][E] in the table dtype, per-evaluation parent lists built by
+// prep_kernel.  A score block owns 64 effects (one per lane) of one
+// evaluation and splits the S children over its 4 waves; every wave streams
+// the table rows of its children's permissible parents (one coalesced
+// 64-lane row segment per parent) and keeps the per-child sum of logs as a
+// running PRODUCT (one multiply per element, one log per child), then the
+// waves merge online log-sum-exp states through LDS.
+#include "nemo_internal.h"
+#include "lbfgsb1.h"
+
+#include <math.h>
+
+namespace nemo {
+
+namespace {
+
+constexpr double kLn2 = 0.69314718055994530942;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// online log-sum-exp state (m = running max, l = sum of exp(c - m))
+__device__ __forceinline__ void lse_push(double& m, double& l, double c) {
+  if (c == -INFINITY) return;
+  if (c > m) {
+    l = l * exp(m - c) + 1.0;
+    m = c;
+  } else {
+    l += exp(c - m);
+  }
+}
+
+__device__ __forceinline__ void lse_merge(double& m, double& l, double m2, double l2) {
+  if (l2 == 0.0) return;
+  if (l == 0.0) { m = m2; l = l2; return; }
+  const double mx = m > m2 ? m : m2;
+  l = l * exp(m - mx) + l2 * exp(m2 - mx);
+  m = mx;
+}
+
+template <typename TT> struct Acc;
+template <> struct Acc<double> {
+  using T = double;
+  __device__ static T term(double s, double v) { return fma(s, v - 1.0, 1.0); }
+  __device__ static T renorm(T p, int& ex) { int e; T r = frexp(p, &e); ex += e; return r; }
+};
+template <> struct Acc<float> {
+  using T = float;
+  __device__ static T term(float s, float v) { return fmaf(s, v - 1.0f, 1.0f); }
+  __device__ static T renorm(T p, int& ex) { int e; T r = frexpf(p, &e); ex += e; return r; }
+};
+
+// ---------------------------------------------------------------------------
+// exp of the staged table (once per model)
+// ---------------------------------------------------------------------------
+template <typename TT>
+__global__ void exp_table_kernel(size_t n, const double* __restrict__ t64, TT* __restrict__ out) {
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < n;
+       k += (size_t)gridDim.x * blockDim.x)
+    out[k] = (TT)exp(t64[k]);
+}
+
+// ---------------------------------------------------------------------------
+// prep: per evaluation, per child i, the permissible parents in pi order
+// (nem_order_mcmc.py:62-65; with cap, the last `cap` of them) and their
+// weights; plus the flat (child, list index) pair list for the local optima.
+// grid = batch, block = S rounded up to 64 (S <= 256).
+// ---------------------------------------------------------------------------
+__global__ void prep_kernel(int S, int cap, const int32_t* __restrict__ pos,
+                            const double* __restrict__ w01, int32_t* __restrict__ rows,
+                            double* __restrict__ sw, int32_t* __restrict__ cnt,
+                            int32_t* __restrict__ pairs) {
+  __shared__ int perm[kMaxS];
+  __shared__ int scan[kMaxS];
+  const int b = blockIdx.x;
+  const int i = threadIdx.x;
+  if (i < S) perm[i] = 0;
+  __syncthreads();
+  int pi = 0;
+  if (i < S) {
+    pi = pos[(size_t)b * S + i];
+    pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);  // malformed input must not fault
+    perm[pi] = i;
+  }
+  __syncthreads();
+  int lo = 0, n = 0;
+  if (i < S) {
+    lo = (cap > 0 && pi > cap) ? pi - cap : 0;
+    n = pi - lo;
+    int32_t* r = rows + ((size_t)b * S + i) * S;
+    double* w = sw + ((size_t)b * S + i) * S;
+    const double* wr = w01 + ((size_t)b * S + i) * S;
+    for (int t = 0; t < n; ++t) {
+      const int j = perm[lo + t];
+      r[t] = j;
+      w[t] = wr[j];
+    }
+    cnt[(size_t)b * S + i] = n;
+  }
+  if (pairs == nullptr) return;
+  scan[i] = (i < S) ? n : 0;
+  __syncthreads();
+  for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+    const int v = (i >= o) ? scan[i - o] : 0;
+    __syncthreads();
+    scan[i] += v;
+    __syncthreads();
+  }
+  if (i < S) {
+    int32_t* pr = pairs + (size_t)b * S * S + (scan[i] - n);
+    for (int t = 0; t < n; ++t) pr[t] = (i << 16) | t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// score: one evaluation x 64 effects per block, children split over waves.
+// grid = (ntiles, batch), block = kScoreWaves * 64.
+// ---------------------------------------------------------------------------
+template <typename TT, bool RENORM>
+__global__ __launch_bounds__(kScoreWaves * kWave) void score_kernel(
+    int S, int E, int ntiles, const TT* __restrict__ eT, const TT* __restrict__ U,
+    const int32_t* __restrict__ rows, const double* __restrict__ sw,
+    const int32_t* __restrict__ cnt, double* __restrict__ partial, double* __restrict__ cs_out,
+    double* __restrict__ cells, double* __restrict__ ow) {
+  using A = Acc<TT>;
+  using PT = typename A::T;
+  __shared__ double sm_m[kScoreWaves][kWave];
+  __shared__ double sm_l[kScoreWaves][kWave];
+  __shared__ double sm_cs[kWave];
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int e = tile * kTileCols + lane;
+  const bool valid = e < E;
+  const int ec = valid ? e : E - 1;
+  double* park = cells ? cells : ow;  // where cell values wait for the ow pass
+
+  double m = -INFINITY, l = 0.0;
+  for (int i = w; i < S; i += kScoreWaves) {
+    const int n = __builtin_amdgcn_readfirstlane(cnt[(size_t)b * S + i]);
+    const int32_t* rp = rows + ((size_t)b * S + i) * S;
+    const double* wp = sw + ((size_t)b * S + i) * S;
+    const TT* base = eT + (size_t)i * S * E + ec;
+    PT prod = (PT)1;
+    int expo = 0;
+    int t = 0;
+    for (; t + 8 <= n; t += 8) {
+      int jj[8];
+      double ss[8];
+      TT vv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        jj[k] = rp[t + k];
+        ss[k] = wp[t + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) vv[k] = base[(size_t)jj[k] * E];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        prod *= A::term((PT)ss[k], vv[k]);
+        if (RENORM && (k & 3) == 3) prod = A::renorm(prod, expo);
+      }
+    }
+    for (; t < n; ++t) {
+      const int j = rp[t];
+      prod *= A::term((PT)wp[t], base[(size_t)j * E]);
+      if (RENORM) prod = A::renorm(prod, expo);
+    }
+    double cell = (double)U[(size_t)i * E + ec] + log((double)prod);
+    if (RENORM) cell += (double)expo * kLn2;
+    if (park && valid) park[((size_t)b * (S + 1) + i) * E + e] = cell;
+    lse_push(m, l, cell);
+  }
+  sm_m[w][lane] = m;
+  sm_l[w][lane] = l;
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int k = 1; k < kScoreWaves; ++k) lse_merge(m, l, sm_m[k][lane], sm_l[k][lane]);
+    const double cnull = (double)U[(size_t)S * E + ec];  // row S: attached to nothing
+    if (park && valid) park[((size_t)b * (S + 1) + S) * E + e] = cnull;
+    lse_push(m, l, cnull);
+    const double cs = m + log(l);
+    sm_cs[lane] = cs;
+    if (cs_out && valid) cs_out[(size_t)b * E + e] = cs;
+    const double part = wave_sum(valid ? cs : 0.0);
+    if (lane == 0) partial[(size_t)b * ntiles + tile] = part;
+  }
+  if (ow == nullptr) return;
+  __syncthreads();
+  const double cs = sm_cs[lane];
+  if (!valid) return;
+  for (int i = w; i <= S; i += kScoreWaves) {
+    const size_t k = ((size_t)b * (S + 1) + i) * E + e;
+    ow[k] = exp(park[k] - cs);
+  }
+}
+
+// ll[b] = sum over tiles (fixed order: bitwise reproducible)
+__global__ void finalize_kernel(int batch, int ntiles, const double* __restrict__ partial,
+                                double* __restrict__ ll) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double s = 0.0;
+  for (int t = 0; t < ntiles; ++t) s += partial[(size_t)b * ntiles + t];
+  ll[b] = s;
+}
+
+// ---------------------------------------------------------------------------
+// grouped (reuse) score: CB evaluations share every table row a block reads.
+// prep_group: for group g and child i, the parents any member needs (ascending
+// j) and a [t][CB] weight block (0 where the member has no such parent).
+// ---------------------------------------------------------------------------
+template <int CB>
+__global__ void prep_group_kernel(int S, int batch, int cap, const int32_t* __restrict__ pos,
+                                  const double* __restrict__ w01, int32_t* __restrict__ rows,
+                                  double* __restrict__ sw, int32_t* __restrict__ cnt) {
+  __shared__ int sp[CB][kMaxS];
+  const int g = blockIdx.x;
+  const int i = threadIdx.x;
+  const int b0 = g * CB;
+  for (int q = 0; q < CB; ++q)
+    if (i < S) sp[q][i] = (b0 + q < batch) ? pos[(size_t)(b0 + q) * S + i] : 0;
+  __syncthreads();
+  if (i >= S) return;
+  int32_t* r = rows + ((size_t)g * S + i) * S;
+  double* w = sw + ((size_t)g * S + i) * S * CB;
+  int t = 0;
+  for (int j = 0; j < S; ++j) {
+    if (j == i) continue;
+    bool any = false;
+    double wt[CB];
+#pragma unroll
+    for (int q = 0; q < CB; ++q) {
+      const int gap = sp[q][i] - sp[q][j];
+      const bool ok = (b0 + q < batch) && gap > 0 && (cap == 0 || gap <= cap);
+      wt[q] = ok ? w01[((size_t)(b0 + q) * S + i) * S + j] : 0.0;
+      any |= ok;
+    }
+    if (!any) continue;
+    r[t] = j;
+#pragma unroll
+    for (int q = 0; q < CB; ++q) w[(size_t)t * CB + q] = wt[q];
+    ++t;
+  }
+  cnt[(size_t)g * S + i] = t;
+}
+
+// grid = (ntiles, ngroups), block = GW waves; dynamic LDS: GW * (S-1) * CB
+// doubles of weights (wave-private), reused for the LSE merge.
+template <typename TT, int CB, int GW>
+__global__ __launch_bounds__(GW * kWave) void score_group_kernel(
+    int S, int E, int ntiles, int batch, const TT* __restrict__ eT, const TT* __restrict__ U,
+    const int32_t* __restrict__ rows, const double* __restrict__ sw,
+    const int32_t* __restrict__ cnt, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tile = blockIdx.x;
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int e = tile * kTileCols + lane;
+  const bool valid = e < E;
+  const int ec = valid ? e : E - 1;
+  double* wl = lds + (size_t)w * (S - 1) * CB;
+  double m[CB], l[CB];
+#pragma unroll
+  for (int q = 0; q < CB; ++q) { m[q] = -INFINITY; l[q] = 0.0; }
+  for (int i = w; i < S; i += GW) {
+    const int n = __builtin_amdgcn_readfirstlane(cnt[(size_t)g * S + i]);
+    const int32_t* rp = rows + ((size_t)g * S + i) * S;
+    const double* wp = sw + ((size_t)g * S + i) * S * CB;
+    for (int k = lane; k < n * CB; k += kWave) wl[k] = wp[k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const TT* base = eT + (size_t)i * S * E + ec;
+    double prod[CB];
+#pragma unroll
+    for (int q = 0; q < CB; ++q) prod[q] = 1.0;
+    int t = 0;
+    for (; t + 4 <= n; t += 4) {
+      double vv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) vv[k] = (double)base[(size_t)rp[t + k] * E];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double wv = vv[k] - 1.0;
+#pragma unroll
+        for (int q = 0; q < CB; ++q) prod[q] *= fma(wl[(t + k) * CB + q], wv, 1.0);
+      }
+    }
+    for (; t < n; ++t) {
+      const double wv = (double)base[(size_t)rp[t] * E] - 1.0;
+#pragma unroll
+      for (int q = 0; q < CB; ++q) prod[q] *= fma(wl[t * CB + q], wv, 1.0);
+    }
+    const double u = (double)U[(size_t)i * E + ec];
+#pragma unroll
+    for (int q = 0; q < CB; ++q) lse_push(m[q], l[q], u + log(prod[q]));
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // merge: waves write states over the (now free) weight region
+  double* mm = lds;                       // [GW][CB][64]
+  double* ll = lds + (size_t)GW * CB * kWave;
+#pragma unroll
+  for (int q = 0; q < CB; ++q) {
+    mm[((size_t)w * CB + q) * kWave + lane] = m[q];
+    ll[((size_t)w * CB + q) * kWave + lane] = l[q];
+  }
+  __syncthreads();
+  if (w != 0) return;
+  const double unull = (double)U[(size_t)S * E + ec];
+#pragma unroll
+  for (int q = 0; q < CB; ++q) {
+    for (int k = 1; k < GW; ++k)
+      lse_merge(m[q], l[q], mm[((size_t)k * CB + q) * kWave + lane],
+                ll[((size_t)k * CB + q) * kWave + lane]);
+    lse_push(m[q], l[q], unull);
+    const double cs = m[q] + log(l[q]);
+    const double part = wave_sum(valid ? cs : 0.0);
+    const int b = g * CB + q;
+    if (lane == 0 && b < batch) partial[(size_t)b * ntiles + tile] = part;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LSE over a given cell matrix (utils.compute_ll / calculate_ll)
+// ---------------------------------------------------------------------------
+__global__ void lse_kernel(int rows, int E, int ntiles, const double* __restrict__ cells,
+                           double* __restrict__ partial, double* __restrict__ cs_out,
+                           double* __restrict__ ow) {
+  const int e = blockIdx.x * kWave + threadIdx.x;
+  const bool valid = e < E;
+  const int ec = valid ? e : E - 1;
+  double m = -INFINITY, l = 0.0;
+  for (int i = 0; i < rows; ++i) lse_push(m, l, cells[(size_t)i * E + ec]);
+  const double cs = m + log(l);
+  if (valid && cs_out) cs_out[e] = cs;
+  const double part = wave_sum(valid ? cs : 0.0);
+  if (threadIdx.x == 0) partial[blockIdx.x] = part;
+  if (ow && valid)
+    for (int i = 0; i < rows; ++i) ow[(size_t)i * E + e] = exp(cells[(size_t)i * E + e] - cs);
+}
+
+// ---------------------------------------------------------------------------
+// local optimum: one wave per problem, c kept in registers (NPL per lane)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double expit_d(double x) { return 1.0 / (1.0 + exp(-x)); }
+
+// c = a / b with a = (lv - 1)*ow_k, b = 1 - s*a + s*(lv - 1)
+// (nem_order_mcmc.py:161-164), operation order kept, no contraction.
+__device__ __forceinline__ double local_c(double lv, double owk, double s) {
+#pragma clang fp contract(off)
+  const double a = (lv - 1.0) * owk;
+  const double b = (1.0 - s * a) + s * (lv - 1.0);
+  return a / b;
+}
+
+template <int NPL>
+struct LocalObjective {
+  double c[NPL];  // this lane's share of the c vector, kept in registers
+  double anc;
+  __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
+#pragma clang fp contract(off)
+    const double e0 = expit_d(x0);
+    const double e1 = expit_d(x1);
+    double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NPL; ++q) {
+      p0 += log(c[q] * e0 + 1.0);
+      p1 += log(c[q] * e1 + 1.0);
+    }
+    p0 = wave_sum(p0);
+    p1 = wave_sum(p1);
+    // nem_order_mcmc.py:20-22: (-sum + |ex - anc|) + ex*(1 - ex)
+    f0 = (-p0 + fabs(e0 - anc)) + e0 * (1.0 - e0);
+    f1 = (-p1 + fabs(e1 - anc)) + e1 * (1.0 - e1);
+  }
+};
+
+__device__ __forceinline__ int32_t pack_info(const LbfgsResult& r) {
+  const int nit = r.nit < 4095 ? r.nit : 4095;
+  const int nfev = r.nfev < 32767 ? r.nfev : 32767;
+  return (int32_t)(r.status | (nit << 4) | (nfev << 16));
+}
+
+// pairs of the fused per-step scorer.  grid covers nchains * npairs waves.
+template <typename TT, int NPL>
+__global__ __launch_bounds__(256) void local_opt_pairs_kernel(
+    int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
+    const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
+    const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
+    double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
+    int32_t* __restrict__ info) {
+  const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  if (gw >= nchains * npairs) return;  // uniform per wave
+  const int b = gw / npairs;
+  const int n = gw - b * npairs;
+  const int pk = pairs[(size_t)b * S * S + n];
+  const int i = pk >> 16;
+  const int t = pk & 0xffff;
+  const int k = rows[((size_t)b * S + i) * S + t];
+  const size_t idx = ((size_t)b * S + i) * S + k;
+  const double s = w01[idx];
+  const TT* tv = eT + ((size_t)i * S + k) * E;
+  const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
+  LocalObjective<NPL> obj;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int e = q * kWave + lane;
+    obj.c[q] = (e < E) ? local_c((double)tv[e], owk[e], s) : 0.0;  // padding: log(1) = 0
+  }
+  obj.anc = anc[idx];
+  const LbfgsResult r = lbfgsb1_minimize(obj, s);
+  if (lane == 0) {
+    const double wx = expit_d(r.x);
+    wnew[idx] = wx;
+    wdag[idx] = (wx > 0.5) ? sig1 : sig0;
+    if (info) info[idx] = pack_info(r);
+  }
+}
+
+// generic batch of problems with caller-given c vectors
+template <int NPL>
+__global__ __launch_bounds__(256) void local_opt_generic_kernel(
+    int n, int E, const double* __restrict__ cvec, const double* __restrict__ anc,
+    const double* __restrict__ x0, double* __restrict__ out) {
+  const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  if (gw >= n) return;
+  LocalObjective<NPL> obj;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int e = q * kWave + lane;
+    obj.c[q] = (e < E) ? cvec[(size_t)gw * E + e] : 0.0;
+  }
+  obj.anc = anc[gw];
+  const LbfgsResult r = lbfgsb1_minimize(obj, x0[gw]);
+  if (lane == 0) {
+    out[(size_t)gw * 3 + 0] = r.x;
+    out[(size_t)gw * 3 + 1] = r.f;
+    out[(size_t)gw * 3 + 2] = (double)pack_info(r);
+  }
+}
+
+int npl_for(int E) {
+  const int need = (E + kWave - 1) / kWave;
+  const int sizes[] = {4, 8, 16, 32, 48, 64, 80};
+  for (int v : sizes)
+    if (need <= v) return v;
+  return -1;
+}
+
+}  // namespace
+
+int pairs_per_chain(int S, int cap) {
+  int p = 0;
+  for (int q = 0; q < S; ++q) p += (cap > 0 && q > cap) ? cap : q;
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_exp_table(Ctx& c, const double* d_T64, hipStream_t st) {
+  const size_t n = (size_t)c.S * c.S * c.E;
+  const int blocks = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  if (c.dtype == 0)
+    exp_table_kernel<double><<<blocks, 256, 0, st>>>(n, d_T64, (double*)c.d_eT);
+  else
+    exp_table_kernel<float><<<blocks, 256, 0, st>>>(n, d_T64, (float*)c.d_eT);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                       int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
+                       hipStream_t st) {
+  const int threads = ((c.S + kWave - 1) / kWave) * kWave;
+  prep_kernel<<<batch, threads, 0, st>>>(c.S, cap, d_pos, d_w01, d_rows, d_sw, d_cnt, d_pairs);
+  return hipGetLastError();
+}
+
+static bool needs_renorm(const Ctx& c) {
+  // products of up to S-1 factors in [min(1,e^T), max(1,e^T)]
+  const double bound = c.table_absmax * (double)(c.S - 1);
+  return c.dtype == 0 ? bound > 600.0 : bound > 80.0;
+}
+
+hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* d_sw,
+                        const int32_t* d_cnt, double* d_ll, double* d_cs, double* d_cells,
+                        double* d_ow, hipStream_t st) {
+  const int nt = c.ntiles();
+  dim3 grid(nt, batch);
+  const bool rn = needs_renorm(c);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+    e0 = c.ev_pool[c.ev_used++];
+    e1 = c.ev_pool[c.ev_used++];
+    hipEventRecord(e0, st);
+  }
+#define NEMO_SC(TT, RN)                                                                      \
+  score_kernel<TT, RN><<<grid, kScoreWaves * kWave, 0, st>>>(                                \
+      c.S, c.E, nt, (const TT*)c.d_eT, (const TT*)c.d_U, d_rows, d_sw, d_cnt, c.d_partial,   \
+      d_cs, d_cells, d_ow)
+  if (c.dtype == 0) {
+    if (rn) NEMO_SC(double, true); else NEMO_SC(double, false);
+  } else {
+    if (rn) NEMO_SC(float, true); else NEMO_SC(float, false);
+  }
+#undef NEMO_SC
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  if (e1) {
+    hipEventRecord(e1, st);
+    c.launches++;
+  }
+  finalize_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, nt, c.d_partial, d_ll);
+  return hipGetLastError();
+}
+
+hipError_t launch_prep_group(Ctx& c, int batch, int group, int cap, const int32_t* d_pos,
+                             const double* d_w01, hipStream_t st) {
+  const int threads = ((c.S + kWave - 1) / kWave) * kWave;
+  const int ng = (batch + group - 1) / group;
+  switch (group) {
+    case 4:
+      prep_group_kernel<4><<<ng, threads, 0, st>>>(c.S, batch, cap, d_pos, d_w01, c.d_grows,
+                                                    c.d_gsw, c.d_gcnt);
+      break;
+    case 8:
+      prep_group_kernel<8><<<ng, threads, 0, st>>>(c.S, batch, cap, d_pos, d_w01, c.d_grows,
+                                                    c.d_gsw, c.d_gcnt);
+      break;
+    case 16:
+      prep_group_kernel<16><<<ng, threads, 0, st>>>(c.S, batch, cap, d_pos, d_w01, c.d_grows,
+                                                     c.d_gsw, c.d_gcnt);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int CB, int GW>
+static hipError_t launch_group_t(Ctx& c, int batch, hipStream_t st) {
+  const int nt = c.ntiles();
+  const int ng = (batch + CB - 1) / CB;
+  const size_t wbytes = (size_t)GW * (c.S - 1) * CB * sizeof(double);
+  const size_t mbytes = (size_t)2 * GW * CB * kWave * sizeof(double);
+  const size_t lds = wbytes > mbytes ? wbytes : mbytes;
+  dim3 grid(nt, ng);
+  if (c.dtype == 0)
+    score_group_kernel<double, CB, GW><<<grid, GW * kWave, lds, st>>>(
+        c.S, c.E, nt, batch, (const double*)c.d_eT, (const double*)c.d_U, c.d_grows, c.d_gsw,
+        c.d_gcnt, c.d_partial);
+  else
+    score_group_kernel<float, CB, GW><<<grid, GW * kWave, lds, st>>>(
+        c.S, c.E, nt, batch, (const float*)c.d_eT, (const float*)c.d_U, c.d_grows, c.d_gsw,
+        c.d_gcnt, c.d_partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStream_t st) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+    e0 = c.ev_pool[c.ev_used++];
+    e1 = c.ev_pool[c.ev_used++];
+    hipEventRecord(e0, st);
+  }
+  hipError_t err;
+  switch (group) {
+    case 4: err = launch_group_t<4, 4>(c, batch, st); break;
+    case 8: err = launch_group_t<8, 4>(c, batch, st); break;
+    case 16: err = launch_group_t<16, 2>(c, batch, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (err != hipSuccess) return err;
+  if (e1) {
+    hipEventRecord(e1, st);
+    c.launches++;
+  }
+  finalize_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, c.ntiles(), c.d_partial, d_ll);
+  return hipGetLastError();
+}
+
+hipError_t launch_lse(Ctx& c, int rows, const double* d_cells, double* d_ll, double* d_cs,
+                      double* d_ow, hipStream_t st) {
+  const int nt = c.ntiles();
+  lse_kernel<<<nt, kWave, 0, st>>>(rows, c.E, nt, d_cells, c.d_partial, d_cs, d_ow);
+  finalize_kernel<<<1, 64, 0, st>>>(1, nt, c.d_partial, d_ll);
+  return hipGetLastError();
+}
+
+template <typename TT>
+static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
+                                const int32_t* d_rows, const double* d_w01, const double* d_anc,
+                                const double* d_ow, double sig0, double sig1, double* d_wnew,
+                                double* d_wdag, int32_t* d_info, hipStream_t st) {
+  const size_t waves = (size_t)nchains * npairs;
+  const int blocks = (int)((waves + 3) / 4);
+  const TT* eT = (const TT*)c.d_eT;
+#define NEMO_LP(NPL)                                                                          \
+  local_opt_pairs_kernel<TT, NPL><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT,      \
+                                                          d_pairs, d_rows, d_w01, d_anc, d_ow, \
+                                                          sig0, sig1, d_wnew, d_wdag, d_info)
+  switch (npl_for(c.E)) {
+    case 4: NEMO_LP(4); break;
+    case 8: NEMO_LP(8); break;
+    case 16: NEMO_LP(16); break;
+    case 32: NEMO_LP(32); break;
+    case 48: NEMO_LP(48); break;
+    case 64: NEMO_LP(64); break;
+    case 80: NEMO_LP(80); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef NEMO_LP
+  return hipGetLastError();
+}
+
+hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
+                                  const int32_t* d_rows, const double* d_w01, const double* d_anc,
+                                  const double* d_ow, double sig0, double sig1, double* d_wnew,
+                                  double* d_wdag, int32_t* d_info, hipStream_t st) {
+  if (nchains * npairs == 0) return hipSuccess;
+  if (c.dtype == 0)
+    return local_pairs_t<double>(c, nchains, npairs, d_pairs, d_rows, d_w01, d_anc, d_ow, sig0,
+                                 sig1, d_wnew, d_wdag, d_info, st);
+  return local_pairs_t<float>(c, nchains, npairs, d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1,
+                              d_wnew, d_wdag, d_info, st);
+}
+
+hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
+                                    const double* d_x0, double* d_out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const int blocks = (n + 3) / 4;
+#define NEMO_LG(NPL) \
+  local_opt_generic_kernel<NPL><<<blocks, 256, 0, st>>>(n, c.E, d_c, d_anc, d_x0, d_out)
+  switch (npl_for(c.E)) {
+    case 4: NEMO_LG(4); break;
+    case 8: NEMO_LG(8); break;
+    case 16: NEMO_LG(16); break;
+    case 32: NEMO_LG(32); break;
+    case 48: NEMO_LG(48); break;
+    case 64: NEMO_LG(64); break;
+    case 80: NEMO_LG(80); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef NEMO_LG
+  return hipGetLastError();
+}
+
+}  // namespace nemo

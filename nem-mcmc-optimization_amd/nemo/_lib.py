@@ -1,0 +1,105 @@
+"""ctypes binding of ``libnemo.so`` (the C-ABI declared in include/nemo.h).
+
+Loading order matters on ROCm: PyTorch ships its own ``libamdhip64.so`` and
+links it by the unversioned name, so when torch is importable it is imported
+first and our library (NEEDED libamdhip64.so.7) resolves to the runtime already
+in the process instead of pulling in a second copy.
+
+There is no CPU fallback: if the library or a GPU is missing, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_LIB = None
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnemo.so")
+
+NEMO_F64, NEMO_F32 = 0, 1
+NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT = 0, -1, -2, -3, -5
+
+_i32p = C.POINTER(C.c_int32)
+_f64p = C.POINTER(C.c_double)
+_vp = C.c_void_p
+
+# (name, restype, argtypes) -- one line per symbol of include/nemo.h
+SIGNATURES = [
+    ("nemo_last_error", C.c_char_p, []),
+    ("nemo_version", C.c_int, []),
+    ("nemo_device_count", C.c_int, [_i32p]),
+    ("nemo_ctx_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    ("nemo_ctx_destroy", None, [_vp]),
+    ("nemo_reserve", C.c_int, [_vp, C.c_int, C.c_int]),
+    ("nemo_stage_tables", C.c_int, [_vp, _f64p, _f64p]),
+    ("nemo_score", C.c_int, [_vp, C.c_int, _i32p, _f64p, C.c_int, _f64p, _f64p, _f64p, _f64p]),
+    ("nemo_score_dev", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp]),
+    ("nemo_score_group_dev", C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int, _vp, _vp]),
+    ("nemo_lse", C.c_int, [_vp, C.c_int, _f64p, _f64p, _f64p, _f64p]),
+    ("nemo_local_opt", C.c_int, [_vp, C.c_int, _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _i32p, _i32p]),
+    ("nemo_optimal_weights", C.c_int, [_vp, C.c_int, _i32p, _f64p, _f64p, C.c_double, C.c_double,
+                                        C.c_int, _f64p, _f64p, _f64p, _i32p]),
+    ("nemo_optimal_weights_dev", C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_double,
+                                            C.c_int, _vp, _vp, _vp, _vp, _vp]),
+    ("nemo_fetch_order_weights", C.c_int, [_vp, C.c_int, _f64p]),
+    ("nemo_timing_enable", C.c_int, [_vp, C.c_int]),
+    ("nemo_timing_read", C.c_int, [_vp, _f64p, _i32p]),
+]
+
+
+class NemoError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
+def lib_path() -> str:
+    return _PATH
+
+
+def load():
+    """Load (once) and return the ctypes library handle."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(_PATH):
+        raise NemoError(NEMO_ERR_STATE, f"{_PATH} not built: run `python -m nemo.build` "
+                                        "(or __graft_entry__.build()); there is no CPU fallback")
+    try:  # share torch's HIP runtime if torch is present (see module docstring)
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    lib = C.CDLL(_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != NEMO_OK:
+        msg = load().nemo_last_error().decode(errors="replace")
+        raise NemoError(rc, msg)
+
+
+def f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def ptr(a, kind=_f64p):
+    if a is None:
+        return None
+    return a.ctypes.data_as(kind)
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    check(load().nemo_device_count(C.byref(n)))
+    return n.value

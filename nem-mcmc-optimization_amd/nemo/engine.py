@@ -1,0 +1,199 @@
+"""Python face of the C-ABI: one :class:`Engine` per (model, device).
+
+An Engine owns a ``nemo_ctx``: the staged tables exp(T) and U in HBM plus the
+per-batch scratch.  Host-array methods mirror the reference's numerical
+routines batch-wise; ``*_dev`` methods take raw device pointers (e.g. from
+``torch.Tensor.data_ptr()``) for callers that keep inputs resident in HBM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, f64, i32, ptr
+
+_DTYPES = {"f64": _lib.NEMO_F64, "f32": _lib.NEMO_F32}
+
+
+class Engine:
+    """Staged model on one GPU.
+
+    ``U`` (S+1, E) and ``T`` (S, S, E) are the reference's node LR table and
+    score tables (nem.py:49-64).  ``dtype='f32'`` stores exp(T) and U in fp32
+    and runs the per-element products in fp32 (the C5 configuration); logs,
+    log-sum-exp and the effect sum stay fp64.
+    """
+
+    def __init__(self, U, T, device: int = 0, dtype: str = "f64"):
+        lib = _lib.load()
+        U = f64(U)
+        T = f64(T)
+        if T.ndim != 3 or T.shape[0] != T.shape[1]:
+            raise ValueError(f"T must be (S, S, E), got {T.shape}")
+        S, _, E = T.shape
+        if U.shape != (S + 1, E):
+            raise ValueError(f"U must be ({S + 1}, {E}), got {U.shape}")
+        self.S, self.E, self.device, self.dtype = S, E, device, dtype
+        self._ctx = C.c_void_p()
+        check(lib.nemo_ctx_create(device, S, E, _DTYPES[dtype], C.byref(self._ctx)))
+        self._fin = weakref.finalize(self, lib.nemo_ctx_destroy, self._ctx)
+        check(lib.nemo_stage_tables(self._ctx, ptr(U), ptr(T)))
+
+    # -- cached engines per model -----------------------------------------
+    @classmethod
+    def for_nem(cls, nem, device: int = 0, dtype: str = "f64") -> "Engine":
+        cache = nem.__dict__.setdefault("_nemo_engines", {})
+        key = (device, dtype)
+        eng = cache.get(key)
+        if eng is None:
+            eng = cls(nem.U, nem.get_score_tensor(), device=device, dtype=dtype)
+            cache[key] = eng
+        return eng
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def close(self):
+        self._fin()
+
+    def reserve(self, max_batch: int, max_chains: int = 0):
+        check(_lib.load().nemo_reserve(self._ctx, int(max_batch), int(max_chains)))
+
+    # -- A4 + A5 -----------------------------------------------------------
+    def score(self, pos, w01, cap: int = 0, want_cs=False, want_cells=False, want_ow=False):
+        """Batched order scores.  pos (B, S) int, w01 (B, S, S) mapped weights.
+        Returns ll (B,) or a dict with the requested extras."""
+        pos = i32(np.atleast_2d(pos))
+        b = pos.shape[0]
+        w01 = f64(w01).reshape(b, self.S, self.S)
+        ll = np.empty(b)
+        cs = np.empty((b, self.E)) if want_cs else None
+        cells = np.empty((b, self.S + 1, self.E)) if want_cells else None
+        ow = np.empty((b, self.S + 1, self.E)) if want_ow else None
+        check(_lib.load().nemo_score(self._ctx, b, ptr(pos, _lib._i32p), ptr(w01), int(cap), ptr(ll),
+                                     ptr(cs), ptr(cells), ptr(ow)))
+        if not (want_cs or want_cells or want_ow):
+            return ll
+        return {"ll": ll, "cs": cs, "cells": cells, "ow": ow}
+
+    def score_dev(self, batch, d_pos, d_w01, d_ll, cap=0, stream=None, group=1):
+        """Enqueue a batched evaluation on device pointers (no sync)."""
+        lib = _lib.load()
+        if group == 1:
+            check(lib.nemo_score_dev(self._ctx, int(batch), d_pos, d_w01, int(cap), d_ll,
+                                     None, None, None, stream))
+        else:
+            check(lib.nemo_score_group_dev(self._ctx, int(batch), int(group), d_pos, d_w01,
+                                           int(cap), d_ll, stream))
+
+    # -- utils.compute_ll / calculate_ll on a given cell matrix ------------
+    def lse(self, cells, want_ow=False):
+        cells = f64(cells)
+        rows = cells.shape[0]
+        ll = np.empty(1)
+        cs = np.empty(self.E)
+        ow = np.empty_like(cells) if want_ow else None
+        check(_lib.load().nemo_lse(self._ctx, rows, ptr(cells), ptr(ll), ptr(cs), ptr(ow)))
+        return float(ll[0]), cs, ow
+
+    # -- A8 core -------------------------------------------------------------
+    def local_opt(self, c, anc, x0):
+        c = f64(np.atleast_2d(c))
+        n = c.shape[0]
+        anc = f64(np.broadcast_to(anc, (n,)))
+        x0 = f64(np.broadcast_to(x0, (n,)))
+        xs, fs = np.empty(n), np.empty(n)
+        nit, nfev, st = (np.empty(n, dtype=np.int32) for _ in range(3))
+        check(_lib.load().nemo_local_opt(self._ctx, n, ptr(c), ptr(anc), ptr(x0), ptr(xs), ptr(fs),
+                                         ptr(nit, _lib._i32p), ptr(nfev, _lib._i32p),
+                                         ptr(st, _lib._i32p)))
+        return xs, fs, nit, nfev, st
+
+    # -- A6 fused step -------------------------------------------------------
+    def optimal_weights(self, pos, w01, anc, w_prev, sig0, sig1, cap: int = 0, raise_on_fail=True):
+        """One get_optimal_weights(init=True, max_iter=1) per chain.
+
+        Returns (w_new, ll1, ll_dag, info): w_new is ``w_prev`` with every
+        permissible entry replaced by expit(x*)."""
+        pos = i32(np.atleast_2d(pos))
+        n = pos.shape[0]
+        w01 = f64(w01).reshape(n, self.S, self.S)
+        anc = f64(anc).reshape(n, self.S, self.S)
+        w_new = np.array(w_prev, dtype=np.float64, copy=True).reshape(n, self.S, self.S)
+        ll1, lld = np.empty(n), np.empty(n)
+        info = np.empty((n, self.S, self.S), dtype=np.int32)
+        rc = _lib.load().nemo_optimal_weights(self._ctx, n, ptr(pos, _lib._i32p), ptr(w01), ptr(anc),
+                                              float(sig0), float(sig1), int(cap), ptr(w_new), ptr(ll1),
+                                              ptr(lld), ptr(info, _lib._i32p))
+        if rc == _lib.NEMO_ERR_OPT and not raise_on_fail:
+            return w_new, ll1, lld, info
+        if rc == _lib.NEMO_ERR_OPT:
+            # the reference raises a plain Exception (nem_order_mcmc.py:168-169)
+            raise Exception(_lib.load().nemo_last_error().decode())
+        check(rc)
+        return w_new, ll1, lld, info
+
+    def order_weights(self, chain: int = 0) -> np.ndarray:
+        out = np.empty((self.S + 1, self.E))
+        check(_lib.load().nemo_fetch_order_weights(self._ctx, int(chain), ptr(out)))
+        return out
+
+    # -- timing of the score kernel ------------------------------------------
+    def timing(self, enable: bool):
+        check(_lib.load().nemo_timing_enable(self._ctx, 1 if enable else 0))
+
+    def timing_read(self):
+        ms = C.c_double(0.0)
+        n = C.c_int32(0)
+        check(_lib.load().nemo_timing_read(self._ctx, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+
+_LSE_ENGINES = {}
+
+
+def lse_ll(cells: np.ndarray, device: int = 0) -> float:
+    """sum_e logsumexp over rows, on the GPU (utils.compute_ll)."""
+    cells = f64(cells)
+    rows, e = cells.shape
+    eng = _LSE_ENGINES.get((e, device))
+    if eng is None:
+        eng = _LseEngine(e, device)
+        _LSE_ENGINES[(e, device)] = eng
+    return eng.ll(cells)
+
+
+class _LseEngine:
+    """A table-less context used only for the LSE kernel."""
+
+    def __init__(self, E, device):
+        lib = _lib.load()
+        self.E = E
+        self._ctx = C.c_void_p()
+        check(lib.nemo_ctx_create(device, 2, E, _lib.NEMO_F64, C.byref(self._ctx)))
+        self._fin = weakref.finalize(self, lib.nemo_ctx_destroy, self._ctx)
+
+    def ll(self, cells, want=False):
+        rows = cells.shape[0]
+        ll = np.empty(1)
+        cs = np.empty(self.E)
+        ow = np.empty_like(cells) if want else None
+        check(_lib.load().nemo_lse(self._ctx, rows, ptr(cells), ptr(ll), ptr(cs), ptr(ow)))
+        if want:
+            return float(ll[0]), cs, ow
+        return float(ll[0])
+
+
+def lse_full(cells: np.ndarray, device: int = 0):
+    """(ll, cs, order_weights) of a given cell matrix, on the GPU."""
+    cells = f64(cells)
+    e = cells.shape[1]
+    eng = _LSE_ENGINES.get((e, device))
+    if eng is None:
+        eng = _LseEngine(e, device)
+        _LSE_ENGINES[(e, device)] = eng
+    return eng.ll(cells, want=True)

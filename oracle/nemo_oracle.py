@@ -1,0 +1,266 @@
+"""ORACLE -- test infrastructure only.  Never imported by the product path.
+
+A CPU (numpy/scipy) restatement of the reference's order-score hot path,
+MrGreyPanda/NEM-MCMC-optimization @ /root/reference, used as the checker for
+the HIP kernels.  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it.
+
+Every function restates one reference function (file:line cited) with the
+same floating-point operation order where that order is observable:
+
+* tables  -- nem.py:25-64 (sequential A additions, ascending S-gene index);
+* order score -- nem_order_mcmc.py:79-93 and utils.py:84-94 (per-parent
+  ``np.log`` accumulation in pi-prefix order, ``np.logaddexp.reduce`` over rows,
+  Python ``sum`` over effects);
+* local optimum -- nem_order_mcmc.py:18-23,160-170, i.e. scipy
+  ``minimize(method='L-BFGS-B', tol=0.01)`` on the penalised local objective.
+  scipy is the reference's own third-party dependency (scipy 1.15.3 in this
+  image; the author's wandb snapshots used 1.11.3/1.12.0) and is called
+  directly here, so the oracle's local optimiser *is* the reference's;
+* sampler -- nem_order_mcmc.py:29-77,172-310 with the entry-point crash at
+  nem_order_mcmc.py:140 replaced by the documented pass-through
+  (SURVEY.md 8(c)): ``opt_weights`` returns the score just computed.
+
+Pinning: tests/test_oracle.py checks this module against the golden vectors
+captured from the reference itself (tests/golden/make_goldens.py, run in the
+build container where /root/reference is importable).
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+from scipy.linalg import inv
+from scipy.optimize import minimize
+from scipy.special import expit
+
+
+# --------------------------------------------------------------------------
+# A1/A2 -- score tables (nem.py:25-64)
+# --------------------------------------------------------------------------
+def base_scores(node, d, a, b):
+    """nem.py:25-34: where(D[node]==1, 0, B) then += where(D[m]==1, A, 0) for
+    every other S-gene m in ascending order."""
+    score = np.where(d[node, :] == 1, 0, b)
+    for m in range(d.shape[0]):
+        if m != node:
+            score = score + np.where(d[m, :] == 1, a, 0)
+    return score
+
+
+def score_tensor(d, a, b):
+    """nem.py:36-54 as one (S, S, E) tensor T[i, j, e]."""
+    s, e = d.shape
+    t = np.empty((s, s, e))
+    for i in range(s):
+        for m in range(s):
+            t[i, m] = base_scores(i, d, a, b) if m == i else np.where(d[m] == 0, b, -a)
+    return t
+
+
+def node_lr_table(t, d, a):
+    """nem.py:56-64."""
+    s = t.shape[0]
+    null_row = np.zeros(d.shape[1])
+    for i in range(s):  # row-by-row accumulation, like ndarray.sum(axis=0)
+        null_row = null_row + np.where(d[i] == 0, 0, a)
+    return np.vstack([t[i, i] for i in range(s)] + [null_row])
+
+
+# --------------------------------------------------------------------------
+# A3 -- permissible parents (nem_order_mcmc.py:54-77)
+# --------------------------------------------------------------------------
+def parents_of(perm, cap=0):
+    """parents[i] = pi[:pos(i)] in order; with a cap, only the last ``cap``
+    entries (build-defined C5 extension)."""
+    perm = np.asarray(perm)
+    out = []
+    for i in range(len(perm)):
+        p = int(np.where(perm == i)[0][0])
+        lo = max(0, p - cap) if cap else 0
+        out.append(perm[lo:p])
+    return out
+
+
+# --------------------------------------------------------------------------
+# A4/A5 -- order score (nem_order_mcmc.py:79-93, utils.py:84-94)
+# --------------------------------------------------------------------------
+def cell_ratios(u, t, parents, w01):
+    """cell[i] = U[i] + sum_{j in pa(i)} log(1 - w + w * exp(T[i][j])) with the
+    already-mapped weight w = w01[i, j] (the reference maps with expit inside,
+    nem_order_mcmc.py:84-86; methods.py:52-57 passes raw weights)."""
+    cell = np.array(u, dtype=np.float64, copy=True)
+    for i in range(t.shape[0]):
+        for j in parents[i]:
+            w = w01[i][j]
+            cell[i, :] += np.log(1.0 - w + w * np.exp(t[i][j]))
+    return cell
+
+
+def calculate_ll(cell):
+    """nem_order_mcmc.py:89-93 -> (order_weights, ll, column LSE)."""
+    cs = np.logaddexp.reduce(cell, axis=0)
+    ow = np.exp(cell - cs)
+    ll = sum(cs)
+    return ow, ll, cs
+
+
+def order_score(u, t, perm, w01, cap=0):
+    """One order-score evaluation: ll of (perm, already-mapped weights)."""
+    cell = cell_ratios(u, t, parents_of(perm, cap), w01)
+    return calculate_ll(cell)[1]
+
+
+# --------------------------------------------------------------------------
+# A8 -- local optimum (nem_order_mcmc.py:18-23, 160-170)
+# --------------------------------------------------------------------------
+def local_objective(x, c, x_anc):
+    """nem_order_mcmc.py:18-23."""
+    ex = expit(x)
+    return -np.sum(np.log(c * ex + 1.0)) + np.abs(ex - x_anc) + ex * (1.0 - ex)
+
+
+def local_c(t_ik, ow_k, w_ik_raw):
+    """c vector of nem_order_mcmc.py:161-164 (row k of the order weights --
+    the PARENT's row -- exactly as written)."""
+    lv = np.exp(t_ik)
+    a = (lv - 1.0) * ow_k
+    s = expit(w_ik_raw)
+    b = 1.0 - s * a + s * (lv - 1.0)
+    return a / b
+
+
+def local_optimum(c, x_anc, x0):
+    """scipy L-BFGS-B exactly as nem_order_mcmc.py:167 calls it.
+    Returns the scipy OptimizeResult."""
+    res = minimize(local_objective, x0=x0, bounds=[(-float("inf"), float("inf"))],
+                   args=(c, x_anc), method="L-BFGS-B", tol=0.01)
+    return res
+
+
+# --------------------------------------------------------------------------
+# A6/A7/A9 -- sampler (nem_order_mcmc.py:29-310)
+# --------------------------------------------------------------------------
+class OracleSampler:
+    """Restatement of ``NEMOrderMCMC`` with the documented ``opt_weights``
+    pass-through.  Uses the global ``random`` stream, like the reference."""
+
+    def __init__(self, u, t, perm_order, record_local=False):
+        self.u = np.array(u, dtype=np.float64)
+        self.t = t
+        self.s = t.shape[0]
+        self.w = np.zeros((self.s, self.s))
+        self.record_local = record_local
+        self.local_log = []
+        self.permissible(np.asarray(perm_order), init=True, init_value=1.0)
+        self.perm_order = np.asarray(perm_order)
+
+    # nem_order_mcmc.py:54-77
+    def permissible(self, perm, i1=None, i2=None, init=False, init_value=0.5):
+        if not init:
+            self.w[i1] = 0
+            self.w[i2] = 0
+            self.w[:, i1] = 0
+            self.w[:, i2] = 0
+        parents = []
+        for i in range(self.s):
+            p = int(np.where(perm == i)[0][0])
+            pa = perm[:p]
+            parents.append(pa)
+            if init:
+                for j in pa:
+                    self.w[i][j] = init_value
+            elif i1 in pa:
+                self.w[i][i1] = init_value
+            elif i2 in pa:
+                self.w[i][i2] = init_value
+            elif i == i1 or i == i2:
+                for j in pa:
+                    self.w[j][i] = init_value
+        self.parents = parents
+
+    def _mapped(self, weights):
+        """expit on permissible entries only (nem_order_mcmc.py:98-103); the
+        cell-ratio loop reads only those entries."""
+        out = np.array(weights, dtype=np.float64, copy=True)
+        for i in range(self.s):
+            for j in self.parents[i]:
+                out[i][j] = expit(out[i][j])
+        return out
+
+    # nem_order_mcmc.py:172-208 (init=True, max_iter=1, the path method() uses)
+    def optimal_weights(self, use_nem=False):
+        mapped = self._mapped(self.w)
+        cell = cell_ratios(self.u, self.t, self.parents, mapped)
+        ow, ll1, _ = calculate_ll(cell)
+        anc = np.clip(inv(np.identity(self.s) - mapped) - np.identity(self.s), 0, 1)
+        new_w = self.w.copy()
+        for i in range(self.s):
+            for k in self.parents[i]:
+                c = local_c(self.t[i][k], ow[k], self.w[i][k])
+                x0 = expit(self.w[i][k])
+                res = local_optimum(c, anc[i][k], x0)
+                if res.success is False:
+                    raise Exception(f"Minimization not successful, Reason: {res.message}")
+                if self.record_local:
+                    self.local_log.append((i, k, c, anc[i][k], x0, res.x[0], res.nit, res.nfev))
+                new_w[i][k] = expit(res.x[0])
+        self.w = new_w.copy()
+        self.ll1, self.ow, self.anc = ll1, ow, anc
+        dag_w = self.dag_weights(self.w, use_nem)
+        dag_cell = cell_ratios(self.u, self.t, self.parents, self._mapped(dag_w))
+        return calculate_ll(dag_cell)[1]
+
+    @staticmethod
+    def dag_weights(w, use_nem=False):
+        """create_dag / create_nem (nem_order_mcmc.py:210-221)."""
+        dag = 1 * (w > 0.5)
+        if not use_nem:
+            return dag
+        n = dag.shape[0]
+        p, tot = dag.copy(), dag.copy()
+        with np.errstate(over="ignore"):
+            for _ in range(1, n):
+                p = p.dot(dag)
+                tot += p
+        return (tot > 0).astype(int)
+
+    # nem_order_mcmc.py:231-255
+    def new_order(self, curr, swap_prob):
+        perm = curr.copy()
+        if random.random() < swap_prob:
+            i, j = random.sample(range(self.s), 2)
+        else:
+            i = random.randint(0, self.s - 2)
+            j = i + 1
+        i1 = int(np.where(perm == i)[0][0])
+        i2 = int(np.where(perm == j)[0][0])
+        perm[i], perm[j] = perm[j], perm[i]
+        return perm, i1, i2
+
+    # nem_order_mcmc.py:257-310 with opt_weights as pass-through
+    def method(self, swap_prob=0.95, gamma=1, n_iterations=500, use_nem=False):
+        curr = self.optimal_weights(use_nem=use_nem)
+        best = curr
+        curr_perm = self.perm_order
+        best_order = curr_perm
+        traj = {"perm": [], "i1": [], "i2": [], "ll": [], "acc": [], "curr": [curr]}
+        self.all_scores = [curr]
+        for _ in range(n_iterations):
+            perm, i1, i2 = self.new_order(curr_perm, swap_prob)
+            self.permissible(perm, i1, i2, init=False)
+            ll = self.optimal_weights(use_nem=use_nem)
+            self.all_scores.append(ll)
+            acc = random.random() < np.exp(gamma * (ll - curr))
+            if acc:
+                curr, curr_perm = ll, perm
+                if curr > best:
+                    best, best_order = curr, curr_perm.copy()
+            traj["perm"].append(perm)
+            traj["i1"].append(i1)
+            traj["i2"].append(i2)
+            traj["ll"].append(ll)
+            traj["acc"].append(acc)
+            traj["curr"].append(curr)
+        self.best_score, self.best_order, self.traj = best, best_order, traj
+        return best

@@ -1,0 +1,250 @@
+"""Capture golden vectors from the reference implementation.
+
+Runs ONLY in the build container, where the reference is mounted read-only at
+/root/reference (it never travels to the GPU box).  It imports the reference
+modules flat (its __init__.py is broken), with a no-op ``wandb`` stub and the
+documented ``opt_weights`` pass-through, and writes small
+``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
+reference's outputs); no reference source is stored.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+
+Versions at capture: see ``meta.json`` written alongside.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import platform
+import random
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+
+def load_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit(f"{REF} not present: goldens can only be captured in the build container")
+    stub = types.ModuleType("wandb")
+    for name in ("init", "log", "login", "finish"):
+        setattr(stub, name, lambda *a, **k: None)
+    sys.modules.setdefault("wandb", stub)
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    import nem as ref_nem
+    import nem_order_mcmc as ref_mcmc
+    import utils as ref_utils
+
+    def opt_weights_passthrough(self):
+        return ref_utils.compute_ll(self.compute_cell_ratios(
+            self.create_dag(self.parent_weights)[1], self.score_tables))
+
+    ref_mcmc.NEMOrderMCMC.opt_weights = opt_weights_passthrough
+    return ref_nem, ref_mcmc, ref_utils
+
+
+def quiet(fn, *a, **k):
+    """The reference prints every weight pass; silence it."""
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a, **k)
+
+
+def repo_generator():
+    sys.path.insert(0, os.path.join(REPO, "nem-mcmc-optimization_amd"))
+    from nemo import generator
+    return generator
+
+
+def ref_nem_without_diagnostics(ref_nem, ref_utils, adj, end_nodes, errors, s, e, seed=42):
+    """NEM.__init__ minus compute_real_score (nem.py:21-22, diagnostic only and
+    very slow at S>=16): same RNG consumption, same tables."""
+    m = ref_nem.NEM.__new__(ref_nem.NEM)
+    m.num_s, m.num_e, m.adj_matrix = s, e, adj
+    alpha, beta = errors
+    m.real_knockdown_mat = ref_utils.create_real_knockdown_mat(adj, end_nodes)
+    random.seed(seed)
+    m.A = np.log(alpha / (1.0 - beta))
+    m.B = np.log(beta / (1.0 - alpha))
+    m.observed_knockdown_mat = ref_utils.create_observed_knockdown_mat(m.real_knockdown_mat, alpha, beta)
+    m.U = m.get_node_lr_table(m.get_score_tables(m.observed_knockdown_mat))
+    return m
+
+
+def ref_eval(ref_mcmc, m, tables, perm, w_raw, cap=0):
+    """compute_cell_ratios + calculate_ll of the reference on (perm, raw W).
+    With a cap, parents_list is overridden by the last <= cap predecessors."""
+    mc = ref_mcmc.NEMOrderMCMC.__new__(ref_mcmc.NEMOrderMCMC)
+    mc.num_s, mc.num_e, mc.U = m.num_s, m.num_e, m.U.copy()
+    mc.parent_weights = np.zeros((m.num_s, m.num_s))
+    mc.get_permissible_parents(perm, init=True, init_value=1.0)
+    if cap:
+        capped = np.empty(m.num_s, dtype=object)
+        for i, pl in enumerate(mc.parents_list):
+            capped[i] = pl[max(0, len(pl) - cap):]
+        mc.parents_list = capped
+    mc.cell_ratios = mc.compute_cell_ratios(w_raw, tables)
+    ow, ll = mc.calculate_ll()
+    cs = np.logaddexp.reduce(mc.cell_ratios, axis=0)
+    return ll, cs, ow
+
+
+def capture_evals(ref_nem, ref_mcmc, ref_utils, gen, name, s, e, seed, cap, n_eval, keep_ow):
+    net = gen.synthetic_network(s, e, seed)
+    m = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, s, e)
+    tables = m.get_score_tables(m.observed_knockdown_mat)
+    perms, ws, lls, css = [], [], [], []
+    ow0 = None
+    for c in range(n_eval):
+        perm, _pos, w = gen.random_chain_inputs(s, c)
+        ll, cs, ow = ref_eval(ref_mcmc, m, tables, perm, w, cap)
+        perms.append(perm)
+        ws.append(w)
+        lls.append(ll)
+        css.append(cs)
+        if keep_ow and c == 0:
+            ow0 = ow
+    d = m.observed_knockdown_mat.astype(np.uint8)
+    out = dict(S=s, E=e, seed=seed, cap=cap, A=m.A, B=m.B,
+               D_packed=np.packbits(d, axis=None),
+               U_sha256=hashlib.sha256(np.ascontiguousarray(m.U, dtype=np.float64).tobytes()).hexdigest(),
+               perm=np.array(perms), W=np.array(ws), ll=np.array(lls), cs=np.array(css))
+    if ow0 is not None:
+        out["ow0"] = ow0
+    if s <= 16:
+        out["U"] = m.U
+    np.savez_compressed(os.path.join(HERE, f"eval_{name}.npz"), **out)
+    print(f"eval_{name}: S={s} E={e} cap={cap} ll={lls}")
+
+
+def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_local_every=0):
+    """Run the patched reference sampler, recording every proposal and
+    decision (and a sample of local optimisations)."""
+    rec = {"perm": [], "i1": [], "i2": [], "acc": []}
+    local = []
+    cls = ref_mcmc.NEMOrderMCMC
+    orig_new, orig_acc, orig_loc = cls.get_new_order, cls.accepting, cls.calculate_local_optimum
+    counter = {"n": 0}
+
+    def new_order(self, curr, swap_prob=0.95):
+        p, i1, i2 = orig_new(self, curr, swap_prob=swap_prob)
+        rec["perm"].append(p.copy())
+        rec["i1"].append(i1)
+        rec["i2"].append(i2)
+        return p, i1, i2
+
+    def accepting(self, *a):
+        r = orig_acc(self, *a)
+        rec["acc"].append(bool(r[0]))
+        return r
+
+    def local_opt(self, i, k):
+        from scipy.optimize import minimize
+        from scipy.special import expit
+        counter["n"] += 1
+        if record_local_every and counter["n"] % record_local_every == 0:
+            lv = np.exp(self.score_tables[i][k])
+            a = (lv - 1.0) * self.order_weights[k]
+            s = expit(self.parent_weights[i][k])
+            b = 1.0 - s * a + s * (lv - 1.0)
+            c = a / b
+            x0 = expit(self.parent_weights[i][k])
+            res = minimize(ref_mcmc.local_ll_sum_penalized, x0=x0, bounds=[(-float("inf"), float("inf"))],
+                           args=(c, self.ancestor_x[i][k]), method="L-BFGS-B", tol=0.01)
+            out = orig_loc(self, i, k)
+            assert out[0] == expit(res.x)[0]
+            local.append((c, self.ancestor_x[i][k], x0, res.x[0], res.nit, res.nfev, res.fun))
+            return out
+        return orig_loc(self, i, k)
+
+    cls.get_new_order, cls.accepting, cls.calculate_local_optimum = new_order, accepting, local_opt
+    try:
+        mc = cls(m, order)
+        best, _dag = quiet(mc.method, n_iterations=n_iter, gamma=gamma, swap_prob=swap_prob)
+    finally:
+        cls.get_new_order, cls.accepting, cls.calculate_local_optimum = orig_new, orig_acc, orig_loc
+    out = dict(order0=np.asarray(order), gamma=gamma, swap_prob=swap_prob, n_iter=n_iter,
+               perm=np.array(rec["perm"]), i1=np.array(rec["i1"]), i2=np.array(rec["i2"]),
+               acc=np.array(rec["acc"]), all_scores=np.array(mc.all_score_list),
+               curr_scores=np.array(mc.curr_score_list), best_scores=np.array(mc.best_score_list),
+               best_score=best, best_order=np.asarray(mc.best_order), final_W=mc.parent_weights,
+               rng_state_after=np.array(random.getstate()[1], dtype=np.int64))
+    np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), **out)
+    print(f"traj_{name}: best={best} accepts={int(np.sum(rec['acc']))}")
+    if local:
+        e = len(local[0][0])
+        np.savez_compressed(
+            os.path.join(HERE, f"localopt_{name}.npz"),
+            c=np.array([r[0] for r in local]).reshape(-1, e), anc=np.array([r[1] for r in local]),
+            x0=np.array([r[2] for r in local]), xstar=np.array([r[3] for r in local]),
+            nit=np.array([r[4] for r in local]), nfev=np.array([r[5] for r in local]),
+            fun=np.array([r[6] for r in local]))
+        print(f"localopt_{name}: {len(local)} records")
+
+
+def main():
+    import scipy
+    ref_nem, ref_mcmc, ref_utils = load_reference()
+    gen = repo_generator()
+
+    # KAT from the reference's own test (tests/utils.tests.py:11-27): data only.
+    s_mat = np.array([[0, 1, 1, 0, 1, 0], [0, 0, 1, 0, 1, 0], [0, 0, 0, 0, 1, 0],
+                      [0, 0, 1, 0, 1, 0], [0, 0, 0, 0, 0, 0], [0, 0, 0, 0, 1, 0]])
+    e_arr = np.array([0, 1, 2, 3, 4, 5, 0])
+    got = ref_utils.create_real_knockdown_mat(s_mat.tolist(), e_arr.tolist())
+    np.savez_compressed(os.path.join(HERE, "kat_knockdown.npz"), s_mat=s_mat, e_arr=e_arr, expected=got)
+
+    # net2 (C1): full reference constructor
+    adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
+    adj_in = adj.copy()
+    m = quiet(ref_nem.NEM, adj, end, err, s, e)
+    tables = np.array(m.get_score_tables(m.observed_knockdown_mat))
+    order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+    np.savez_compressed(
+        os.path.join(HERE, "net2_tables.npz"), adj_in=adj_in, adj_after=adj, end_nodes=end, errors=err,
+        S=s, E=e, D=m.observed_knockdown_mat.astype(np.uint8), D_real=m.real_knockdown_mat.astype(np.uint8),
+        A=m.A, B=m.B, U=m.U, T=tables, order0=order,
+        rng_state_after_nem=np.array(random.getstate()[1], dtype=np.int64),
+        real_order_ll=m.real_order_ll, real_ll=m.real_ll, obs_order_ll=m.obs_order_ll, obs_ll=m.obs_ll)
+    # eval fixtures on net2
+    perms, ws, lls, css = [], [], [], []
+    for c in range(8):
+        perm, _pos, w = gen.random_chain_inputs(s, c)
+        ll, cs, ow = ref_eval(ref_mcmc, m, list(tables), perm, w)
+        perms.append(perm), ws.append(w), lls.append(ll), css.append(cs)
+        if c == 0:
+            ow0 = ow
+    np.savez_compressed(os.path.join(HERE, "eval_net2.npz"), S=s, E=e, cap=0, perm=np.array(perms),
+                        W=np.array(ws), ll=np.array(lls), cs=np.array(css), ow0=ow0)
+
+    # C1 trajectory: net2, 200 steps, gamma = 2S/E, swap_prob 0.90 (main.py:66-70)
+    random.setstate(random.getstate())  # state is the post-NEM state, as in main()
+    capture_traj(ref_mcmc, m, order, 2.0 * s / e, 0.90, 200, "net2_200", record_local_every=5)
+
+    # synthetic evals: C2, C3, C5 (cap 6, reference fp64)
+    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C2", 16, 500, 0, 0, 8, True)
+    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 4, True)
+    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C5cap", 128, 5000, 0, 6, 3, False)
+
+    # C2 trajectory, 20 steps (default swap_prob 0.95, gamma = 2S/E)
+    net = gen.synthetic_network(16, 500, 0)
+    mc2 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 16, 500)
+    order2 = ref_utils.initial_order_guess(mc2.observed_knockdown_mat)
+    capture_traj(ref_mcmc, mc2, order2, 2.0 * 16 / 500, 0.95, 20, "C2_20", record_local_every=7)
+
+    meta = dict(python=platform.python_version(), numpy=np.__version__, scipy=scipy.__version__,
+                machine=platform.machine(), processor=platform.processor(), reference=REF)
+    with open(os.path.join(HERE, "meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+    print(meta)
+
+
+if __name__ == "__main__":
+    main()

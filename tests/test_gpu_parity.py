@@ -1,0 +1,246 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the reference's
+golden vectors and the pinned oracle.  Tolerances (north_star): log-scores
+within 1e-6 absolute in fp64; the fp32 table path (C5) within 1e-6 relative;
+accepted-move indices of the sampler identical under the reference's seed."""
+import random
+
+import numpy as np
+import pytest
+from conftest import golden
+from scipy.special import expit
+
+import nemo_oracle as no
+from nemo import NEM, generator, utils
+from nemo.engine import Engine, lse_full
+
+pytestmark = pytest.mark.gpu
+
+LL_TOL = 1e-6
+
+
+def _pos(perm):
+    perm = np.asarray(perm)
+    pos = np.empty(len(perm), dtype=np.int32)
+    pos[perm] = np.arange(len(perm))
+    return pos
+
+
+def _unpack_d(z):
+    s, e = int(z["S"]), int(z["E"])
+    return np.unpackbits(z["D_packed"])[: s * e].reshape(s, e).astype(np.float64)
+
+
+@pytest.fixture(scope="module")
+def net2_engine():
+    z = golden("net2_tables.npz")
+    return Engine(z["U"], z["T"]), z
+
+
+@pytest.fixture(scope="module")
+def c3_model():
+    m = generator.synthetic_nem(64, 2000, 0)
+    return m, Engine.for_nem(m)
+
+
+def _golden_batch(z):
+    pos = np.array([_pos(p) for p in z["perm"]])
+    return pos, expit(z["W"])
+
+
+def test_score_net2_golden(net2_engine):
+    eng, t = net2_engine
+    z = golden("eval_net2.npz")
+    pos, w01 = _golden_batch(z)
+    out = eng.score(pos, w01, want_cs=True, want_cells=True, want_ow=True)
+    assert np.max(np.abs(out["ll"] - z["ll"])) <= 1e-9
+    assert np.max(np.abs(out["cs"] - z["cs"])) <= 1e-11
+    assert np.max(np.abs(out["ow"][0] - z["ow0"])) <= 1e-12
+    for c in range(len(pos)):
+        cell = no.cell_ratios(t["U"], t["T"], no.parents_of(z["perm"][c]), w01[c])
+        assert np.max(np.abs(out["cells"][c] - cell)) <= 1e-11
+    # single-eval calls give the same bits as the batch
+    for c in (0, 5):
+        assert eng.score(pos[c:c + 1], w01[c:c + 1])[0] == out["ll"][c]
+
+
+@pytest.mark.parametrize("name,s,e", [("C2", 16, 500), ("C3", 64, 2000)])
+def test_score_synthetic_golden(name, s, e):
+    z = golden(f"eval_{name}.npz")
+    m = generator.synthetic_nem(s, e, 0)
+    assert np.array_equal(m.observed_knockdown_mat, _unpack_d(z))
+    eng = Engine.for_nem(m)
+    pos, w01 = _golden_batch(z)
+    out = eng.score(pos, w01, want_cs=True, want_ow=True)
+    assert np.max(np.abs(out["ll"] - z["ll"])) <= LL_TOL
+    assert np.max(np.abs(out["cs"] - z["cs"])) <= 1e-9
+    assert np.max(np.abs(out["ow"][0] - z["ow0"])) <= 1e-11
+    np.testing.assert_allclose(out["ow"].sum(axis=1), 1.0, atol=1e-12)
+
+
+def test_score_c5_cap6_f64_and_f32():
+    z = golden("eval_C5cap.npz")
+    m = generator.synthetic_nem(128, 5000, 0)
+    assert np.array_equal(m.observed_knockdown_mat, _unpack_d(z))
+    pos, w01 = _golden_batch(z)
+    e64 = Engine.for_nem(m, dtype="f64")
+    ll64 = e64.score(pos, w01, cap=6)
+    assert np.max(np.abs(ll64 - z["ll"])) <= LL_TOL
+    e64.close()
+    e32 = Engine.for_nem(m, dtype="f32")
+    ll32 = e32.score(pos, w01, cap=6)
+    # fp32 storage and products, fp64 logs / LSE / effect sum
+    assert np.max(np.abs(ll32 - z["ll"]) / np.abs(z["ll"])) <= 1e-6
+    e32.close()
+
+
+def test_full_size_properties_c3(c3_model):
+    m, eng = c3_model
+    s = m.num_s
+    b = 48
+    rng = np.random.default_rng(9)
+    pos = np.array([rng.permutation(s) for _ in range(b)], dtype=np.int32)
+    w01 = expit(rng.uniform(-3, 3, (b, s, s)))
+    ll = eng.score(pos, w01)
+    # deterministic, batch-position invariant
+    assert np.array_equal(eng.score(pos, w01), ll)
+    assert np.array_equal(eng.score(pos[::-1], w01[::-1]), ll[::-1])
+    # zero weights: every cell is U, ll = sum_e logsumexp(U[:, e])
+    ll0 = eng.score(pos[:2], np.zeros((2, s, s)))
+    ref0 = sum(np.logaddexp.reduce(m.U, axis=0))
+    assert np.max(np.abs(ll0 - ref0)) <= 1e-9
+    # oracle on a few of them
+    t = m.get_score_tensor()
+    for c in (0, 17):
+        perm = np.argsort(pos[c])
+        ref = no.order_score(m.U, t, perm, w01[c])
+        assert abs(ll[c] - ref) <= LL_TOL
+
+
+def test_group_kernel_matches_stream(c3_model):
+    import torch
+    m, eng = c3_model
+    s = m.num_s
+    b = 40
+    rng = np.random.default_rng(4)
+    pos = np.array([rng.permutation(s) for _ in range(b)], dtype=np.int32)
+    w01 = expit(rng.uniform(-3, 3, (b, s, s)))
+    ref = eng.score(pos, w01)
+    eng.reserve(b)
+    dpos = torch.from_numpy(pos).cuda()
+    dw = torch.from_numpy(w01).cuda()
+    for g in (1, 4, 8, 16):
+        dll = torch.zeros(b, dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        eng.score_dev(b, dpos.data_ptr(), dw.data_ptr(), dll.data_ptr(), stream=st, group=g)
+        torch.cuda.synchronize()
+        got = dll.cpu().numpy()
+        assert np.max(np.abs(got - ref) / np.abs(ref)) <= 1e-13, g
+
+
+def test_lse_kernel_matches_numpy():
+    rng = np.random.default_rng(2)
+    cells = rng.normal(-50, 20, (33, 300))
+    cells[3, 7] = -np.inf
+    ll, cs, ow = lse_full(cells)
+    ref_cs = np.logaddexp.reduce(cells, axis=0)
+    assert np.max(np.abs(cs - ref_cs)) <= 1e-12
+    assert abs(ll - sum(ref_cs)) <= 1e-9
+    assert np.max(np.abs(ow - np.exp(cells - ref_cs))) <= 1e-12
+    assert abs(utils.compute_ll(cells) - sum(ref_cs)) <= 1e-9
+
+
+@pytest.mark.parametrize("name", ["net2_200", "C2_20"])
+def test_local_opt_vs_scipy_records(name):
+    z = golden(f"localopt_{name}.npz")
+    e = z["c"].shape[1]
+    eng = Engine(np.zeros((3, e)), np.zeros((2, 2, e)))
+    xs, fs, nit, nfev, st = eng.local_opt(z["c"], z["anc"], z["x0"])
+    assert np.all(st <= 1)
+    same = (nit == z["nit"]) & (nfev == z["nfev"])
+    assert same.mean() >= 0.97
+    rel = np.abs(xs - z["xstar"]) / np.maximum(1, np.abs(z["xstar"]))
+    assert np.max(rel[same]) <= 1e-3
+    assert np.array_equal(np.sign(xs), np.sign(z["xstar"]))
+    np.testing.assert_allclose(fs[same], z["fun"][same], rtol=0, atol=1e-6)
+
+
+def _oracle_step_inputs(u, t, perm, w_raw):
+    smp = no.OracleSampler(u, t, perm)
+    smp.w = w_raw.copy()
+    return smp
+
+
+def test_fused_step_vs_oracle_c3(c3_model):
+    """One get_optimal_weights at 64x2000 (2016 local optima) vs the oracle."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m, eng = c3_model
+    t = m.get_score_tensor()
+    rng = np.random.default_rng(12)
+    perm = rng.permutation(m.num_s)
+    smp = NEMOrderMCMC(m, perm, engine=eng)
+    w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
+    smp.parent_weights = w_raw.copy()
+    ora = _oracle_step_inputs(m.U, t, perm, w_raw)
+    ref_dag = ora.optimal_weights()
+    got_dag = smp.get_optimal_weights(init=True)
+    assert abs(smp.ll - ora.ll1) <= LL_TOL
+    mask = smp._mask
+    assert np.array_equal(smp.parent_weights[~mask], ora.w[~mask])
+    dw = np.abs(smp.parent_weights[mask] - ora.w[mask])
+    assert np.mean(dw <= 1e-6) >= 0.97 and np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
+    assert abs(got_dag - ref_dag) <= LL_TOL
+
+
+def _run_sampler(m, order, gamma, swap_prob, n, state):
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    random.setstate(state)
+    smp = NEMOrderMCMC(m, order)
+    best, _ = smp.method(n_iterations=n, gamma=gamma, swap_prob=swap_prob, verbose=False)
+    return smp, best
+
+
+def test_trajectory_net2_200(net2):
+    """C1: 200 MCMC steps on network2 with the reference's seed: identical
+    accepted moves, scores within 1e-6."""
+    m, state = net2
+    z = golden("traj_net2_200.npz")
+    smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
+                             int(z["n_iter"]), state)
+    assert np.array_equal(np.array(smp.accepted), z["acc"])
+    scores = np.array(smp.all_score_list)
+    assert np.max(np.abs(scores - z["all_scores"])) <= LL_TOL
+    assert abs(best - float(z["best_score"])) <= LL_TOL
+    assert np.array_equal(smp.best_order, z["best_order"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_trajectory_c2_20():
+    z = golden("traj_C2_20.npz")
+    m = generator.synthetic_nem(16, 500, 0)
+    state = random.getstate()
+    smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
+                             int(z["n_iter"]), state)
+    assert np.array_equal(np.array(smp.accepted), z["acc"])
+    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
+
+
+def test_edge_cases():
+    # smallest model, E not a multiple of the 64-effect tile, E = 1
+    for s, e in ((2, 1), (3, 65), (5, 130)):
+        m = generator.synthetic_nem(s, e, 1)
+        t = m.get_score_tensor()
+        eng = Engine(m.U, t)
+        rng = np.random.default_rng(s * e)
+        perms = [rng.permutation(s) for _ in range(3)]
+        w01 = expit(rng.uniform(-3, 3, (3, s, s)))
+        ll = eng.score(np.array([_pos(p) for p in perms]), w01)
+        for c in range(3):
+            assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-9
+        # a cap at least S-1 is no cap
+        assert np.array_equal(eng.score(np.array([_pos(p) for p in perms]), w01, cap=s), ll)
+        eng.close()
+    m = generator.synthetic_nem(4, 10, 0)
+    eng = Engine(m.U, m.get_score_tensor())
+    assert eng.score(np.zeros((0, 4), dtype=np.int32), np.zeros((0, 4, 4))).shape == (0,)
+    with pytest.raises(RuntimeError, match="permutation"):
+        eng.score(np.array([[0, 0, 1, 2]]), np.zeros((1, 4, 4)))
