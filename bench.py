@@ -101,7 +101,9 @@ def main():
     d_pos = torch.from_numpy(pos).cuda()
     d_w01 = torch.from_numpy(w01).cuda()
     d_ll = torch.zeros(B, dtype=torch.float64, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    side = torch.cuda.Stream()          # the stream every kernel is launched on
+    torch.cuda.set_stream(side)
+    stream = side.cuda_stream
 
     def step():
         eng.score_dev(B, d_pos.data_ptr(), d_w01.data_ptr(), d_ll.data_ptr(), cap=cap,
@@ -117,7 +119,7 @@ def main():
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
+    ev0.record(side)
     for _ in range(args.steps):
         step()
     if world > 1:
@@ -125,7 +127,7 @@ def main():
         best = d_ll.max().reshape(1)
         allb = [torch.empty_like(best) for _ in range(world)]
         dist.all_gather(allb, best)
-    ev1.record()
+    ev1.record(side)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -14,7 +14,7 @@
  *     (thread-local) explains it; the Python host raises RuntimeError with it;
  *   - host-pointer calls are synchronous (the context stream is synchronised
  *     before return); *_dev calls take device pointers and only enqueue work on
- *     the given stream (hipStream_t passed as void*, NULL = context stream);
+ *     the given stream (hipStream_t passed as void*; NULL = HIP's null stream);
  *   - one context per (device, model); calls on one context must not overlap.
  *
  * Layouts (row-major, C order):
@@ -126,6 +126,9 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
 /* order weights of chain `chain` from the last eval#1 of nemo_optimal_weights:
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
+
+/* ---- tuning knobs (speed only, never results): "xcd_remap" (default 1) -- */
+int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 
 /* ---- timing of the dominant (score) kernel, for bench.py ---------------- */
 int nemo_timing_enable(nemo_ctx* ctx, int enable);

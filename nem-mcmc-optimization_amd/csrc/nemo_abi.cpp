@@ -72,9 +72,9 @@ int check_pos(const int32_t* pos, int batch, int S) {
   return NEMO_OK;
 }
 
-hipStream_t pick(nemo_ctx* ctx, void* stream) {
-  return stream ? (hipStream_t)stream : ctx->c.stream;
-}
+// *_dev entry points run on the caller's stream verbatim: NULL is HIP's null
+// stream (torch's default stream), as in the HIP API itself
+hipStream_t pick(nemo_ctx*, void* stream) { return (hipStream_t)stream; }
 
 }  // namespace
 
@@ -443,6 +443,17 @@ int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
   HIPCHK(hipMemcpyAsync(ow_out, c.d_ow + (size_t)chain * n, n * 8, hipMemcpyDeviceToHost, c.stream));
   HIPCHK(hipStreamSynchronize(c.stream));
   return NEMO_OK;
+}
+
+int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!name) return fail(NEMO_ERR_ARG, "null option name");
+  if (strcmp(name, "xcd_remap") == 0) {
+    ctx->c.xcd_remap = value ? 1 : 0;
+    return NEMO_OK;
+  }
+  return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
 }
 
 // ---------------------------------------------------------------------------

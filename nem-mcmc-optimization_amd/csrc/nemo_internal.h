@@ -22,6 +22,7 @@ struct Ctx {
   int S = 0, E = 0, dtype = 0;     // dtype: 0 f64, 1 f32
   hipStream_t stream = nullptr;
   bool staged = false;
+  int xcd_remap = 1;               // option "xcd_remap": XCD-aware block order
   double table_absmax = 0.0;       // max |T| over off-diagonal rows
   void* d_eT = nullptr;            // exp(T) [S][S][E] (dtype)
   void* d_U = nullptr;             // U [S+1][E] (dtype)

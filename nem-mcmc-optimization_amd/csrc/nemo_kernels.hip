@@ -51,6 +51,19 @@ __device__ __forceinline__ void lse_merge(double& m, double& l, double m2, doubl
   m = mx;
 }
 
+// XCD-aware block order (MI355X_MICROARCH.md: blocks are dealt round-robin to
+// the 8 XCDs, so block L runs on XCD L % 8).  Remap the 1-D block index to a
+// work index so that each XCD receives a CONTIGUOUS range of the tile-major
+// work list: the blocks in flight on one XCD then share the same 64-effect
+// table columns, which stay in that XCD's 4 MB L2.  Bijective for any N;
+// placement only changes speed, never results.
+__device__ __forceinline__ int xcd_work_index(int L, int N, int remap) {
+  if (!remap) return L;
+  const int x = L & 7, k = L >> 3;
+  const int q = N >> 3, r = N & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 template <typename TT> struct Acc;
 template <> struct Acc<double> {
   using T = double;
@@ -127,21 +140,23 @@ __global__ void prep_kernel(int S, int cap, const int32_t* __restrict__ pos,
 
 // ---------------------------------------------------------------------------
 // score: one evaluation x 64 effects per block, children split over waves.
-// grid = (ntiles, batch), block = kScoreWaves * 64.
+// grid = ntiles * batch (1-D, XCD-remapped), block = kScoreWaves * 64.
 // ---------------------------------------------------------------------------
 template <typename TT, bool RENORM>
 __global__ __launch_bounds__(kScoreWaves * kWave) void score_kernel(
     int S, int E, int ntiles, const TT* __restrict__ eT, const TT* __restrict__ U,
     const int32_t* __restrict__ rows, const double* __restrict__ sw,
     const int32_t* __restrict__ cnt, double* __restrict__ partial, double* __restrict__ cs_out,
-    double* __restrict__ cells, double* __restrict__ ow) {
+    double* __restrict__ cells, double* __restrict__ ow, int remap) {
   using A = Acc<TT>;
   using PT = typename A::T;
   __shared__ double sm_m[kScoreWaves][kWave];
   __shared__ double sm_l[kScoreWaves][kWave];
   __shared__ double sm_cs[kWave];
-  const int tile = blockIdx.x;
-  const int b = blockIdx.y;
+  const int batch = (int)gridDim.x / ntiles;
+  const int work = xcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
+  const int tile = work / batch;       // tile-major: consecutive work shares columns
+  const int b = work - tile * batch;
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int e = tile * kTileCols + lane;
@@ -266,10 +281,12 @@ template <typename TT, int CB, int GW>
 __global__ __launch_bounds__(GW * kWave) void score_group_kernel(
     int S, int E, int ntiles, int batch, const TT* __restrict__ eT, const TT* __restrict__ U,
     const int32_t* __restrict__ rows, const double* __restrict__ sw,
-    const int32_t* __restrict__ cnt, double* __restrict__ partial) {
+    const int32_t* __restrict__ cnt, double* __restrict__ partial, int remap) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tile = blockIdx.x;
-  const int g = blockIdx.y;
+  const int ngroups = (int)gridDim.x / ntiles;
+  const int work = xcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
+  const int tile = work / ngroups;
+  const int g = work - tile * ngroups;
   const int lane = threadIdx.x & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int e = tile * kTileCols + lane;
@@ -505,7 +522,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
                         const int32_t* d_cnt, double* d_ll, double* d_cs, double* d_cells,
                         double* d_ow, hipStream_t st) {
   const int nt = c.ntiles();
-  dim3 grid(nt, batch);
+  dim3 grid(nt * batch);
   const bool rn = needs_renorm(c);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
@@ -516,7 +533,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
 #define NEMO_SC(TT, RN)                                                                      \
   score_kernel<TT, RN><<<grid, kScoreWaves * kWave, 0, st>>>(                                \
       c.S, c.E, nt, (const TT*)c.d_eT, (const TT*)c.d_U, d_rows, d_sw, d_cnt, c.d_partial,   \
-      d_cs, d_cells, d_ow)
+      d_cs, d_cells, d_ow, c.xcd_remap)
   if (c.dtype == 0) {
     if (rn) NEMO_SC(double, true); else NEMO_SC(double, false);
   } else {
@@ -563,15 +580,15 @@ static hipError_t launch_group_t(Ctx& c, int batch, hipStream_t st) {
   const size_t wbytes = (size_t)GW * (c.S - 1) * CB * sizeof(double);
   const size_t mbytes = (size_t)2 * GW * CB * kWave * sizeof(double);
   const size_t lds = wbytes > mbytes ? wbytes : mbytes;
-  dim3 grid(nt, ng);
+  dim3 grid(nt * ng);
   if (c.dtype == 0)
     score_group_kernel<double, CB, GW><<<grid, GW * kWave, lds, st>>>(
         c.S, c.E, nt, batch, (const double*)c.d_eT, (const double*)c.d_U, c.d_grows, c.d_gsw,
-        c.d_gcnt, c.d_partial);
+        c.d_gcnt, c.d_partial, c.xcd_remap);
   else
     score_group_kernel<float, CB, GW><<<grid, GW * kWave, lds, st>>>(
         c.S, c.E, nt, batch, (const float*)c.d_eT, (const float*)c.d_U, c.d_grows, c.d_gsw,
-        c.d_gcnt, c.d_partial);
+        c.d_gcnt, c.d_partial, c.xcd_remap);
   return hipGetLastError();
 }
 

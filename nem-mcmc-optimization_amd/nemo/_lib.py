@@ -43,6 +43,7 @@ SIGNATURES = [
     ("nemo_optimal_weights_dev", C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_double,
                                             C.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("nemo_fetch_order_weights", C.c_int, [_vp, C.c_int, _f64p]),
+    ("nemo_set_option", C.c_int, [_vp, C.c_char_p, C.c_int]),
     ("nemo_timing_enable", C.c_int, [_vp, C.c_int]),
     ("nemo_timing_read", C.c_int, [_vp, _f64p, _i32p]),
 ]

@@ -142,6 +142,9 @@ class Engine:
         check(_lib.load().nemo_fetch_order_weights(self._ctx, int(chain), ptr(out)))
         return out
 
+    def set_option(self, name: str, value: int):
+        check(_lib.load().nemo_set_option(self._ctx, name.encode(), int(value)))
+
     # -- timing of the score kernel ------------------------------------------
     def timing(self, enable: bool):
         check(_lib.load().nemo_timing_enable(self._ctx, 1 if enable else 0))

@@ -161,7 +161,8 @@ def test_local_opt_vs_scipy_records(name):
     rel = np.abs(xs - z["xstar"]) / np.maximum(1, np.abs(z["xstar"]))
     assert np.max(rel[same]) <= 1e-3
     assert np.array_equal(np.sign(xs), np.sign(z["xstar"]))
-    np.testing.assert_allclose(fs[same], z["fun"][same], rtol=0, atol=1e-6)
+    # f* at an x* that differs by forward-difference noise (~1e-5 rel.)
+    np.testing.assert_allclose(fs[same], z["fun"][same], rtol=1e-6, atol=1e-6)
 
 
 def _oracle_step_inputs(u, t, perm, w_raw):
