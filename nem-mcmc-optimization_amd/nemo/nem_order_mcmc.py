@@ -36,6 +36,10 @@ SIG1 = float(expit(1.0))   # expit of a binarised "edge" weight
 
 
 class NEMOrderMCMC:
+    # proposal / acceptance stream: the global ``random`` module, as in the
+    # reference; nemo.chains gives each batched chain its own random.Random
+    rng = random
+
     def __init__(self, nem, perm_order, device: int = 0, dtype: str = "f64", cap: int = 0,
                  engine: Engine | None = None):
         """Reference: nem_order_mcmc.py:29-48.
@@ -233,7 +237,7 @@ class NEMOrderMCMC:
     def accepting(self, score, curr_score, gamma, net, curr_net, perm_order, curr_perm_order):
         """Reference: nem_order_mcmc.py:224-229 (one random() draw)."""
         acceptance_rate = np.exp(gamma * (score - curr_score))
-        if random.random() < acceptance_rate:
+        if self.rng.random() < acceptance_rate:
             return True, score, net, perm_order
         return False, curr_score, curr_net, curr_perm_order
 
@@ -241,10 +245,11 @@ class NEMOrderMCMC:
         """Reference: nem_order_mcmc.py:231-255.  i1, i2 are the positions of
         the node LABELS i, j; the swap exchanges POSITIONS i, j (as written)."""
         perm_order = curr_perm_order.copy()
-        if random.random() < swap_prob:
-            i, j = random.sample(range(self.num_s), 2)
+        rng = self.rng
+        if rng.random() < swap_prob:
+            i, j = rng.sample(range(self.num_s), 2)
         else:
-            i = random.randint(0, self.num_s - 2)
+            i = rng.randint(0, self.num_s - 2)
             j = i + 1
         i1 = np.where(perm_order == i)[0][0]
         i2 = np.where(perm_order == j)[0][0]

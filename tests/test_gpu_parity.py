@@ -245,3 +245,22 @@ def test_edge_cases():
     assert eng.score(np.zeros((0, 4), dtype=np.int32), np.zeros((0, 4, 4))).shape == (0,)
     with pytest.raises(RuntimeError, match="permutation"):
         eng.score(np.array([[0, 0, 1, 2]]), np.zeros((1, 4, 4)))
+
+
+def test_chain_batch_equals_single_chains():
+    """Lock-step batching (one fused call for all chains) reproduces each
+    chain's single-chain run driven by the same random stream, bit for bit."""
+    from nemo.chains import ChainBatch
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(16, 500, 0)
+    orders = [np.random.default_rng(k).permutation(16) for k in range(4)]
+    seeds = [11, 12, 13, 14]
+    cb = ChainBatch(m, orders, seeds, swap_prob=0.95)
+    best, best_orders = cb.run(8)
+    for k in range(4):
+        single = NEMOrderMCMC(m, orders[k], engine=cb.engine)
+        single.rng = random.Random(seeds[k])
+        b, _ = single.method(n_iterations=8, gamma=cb.gamma, swap_prob=0.95, verbose=False)
+        assert np.array_equal(np.array(single.accepted), cb.accepted[:, k])
+        assert b == best[k]
+        assert np.array_equal(single.best_order, best_orders[k])
