@@ -127,8 +127,15 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
 
-/* ---- tuning knobs (speed only, never results): "xcd_remap" (default 1) -- */
+/* ---- options -------------------------------------------------------------
+ *   "xcd_remap"  1 (default) XCD-aware block order; speed only
+ *   "score_path" 0 (default) auto: the factored MFMA kernel when the staged
+ *                table has the NEM structure (every off-diagonal row T[.][j]
+ *                shared by all children and two-valued), else the streaming
+ *                kernel; 1 = always stream; 2 = always factored
+ *   "factored"   (get only) 1 if the staged table is factorable */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
+int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 
 /* ---- timing of the dominant (score) kernel, for bench.py ---------------- */
 int nemo_timing_enable(nemo_ctx* ctx, int enable);

@@ -125,7 +125,9 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
   hipStreamSynchronize(c.stream);
   void* bufs[] = {c.d_eT,   c.d_U,    c.d_pos,  c.d_w01,  c.d_anc,     c.d_rows, c.d_sw,
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
-                  c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt};
+                  c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
+                  c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
+                  c.d_fpartial};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -151,6 +153,11 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_ll, nb));
     HIPCHK(dalloc(&c.d_cs, nb * E));
     HIPCHK(dalloc(&c.d_ow, nb * (S + 1) * E));
+    const size_t sp = nemo::factored_spad(c.S);
+    HIPCHK(dalloc(&c.d_fDp, nb * sp * sp));
+    HIPCHK(dalloc(&c.d_fG, nb * sp));
+    HIPCHK(dalloc(&c.d_fperm, nb * sp));
+    HIPCHK(dalloc(&c.d_fpartial, nb * (size_t)nemo::factored_partials(c)));
     c.cap_batch = nb;
   }
   const int nc = std::max(max_chains, 1);
@@ -213,8 +220,63 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
   HIPCHK(hipStreamSynchronize(c.stream));
   HIPCHK(hipFree(d_t64));
   c.table_absmax = amax;
+
+  // factored form: every off-diagonal row j identical for all children and
+  // two-valued (nem.py:44-46 builds exactly that)
+  const int nwords = (int)((E + 63) / 64);
+  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
+  std::vector<double> elo(S), ehi(S);
+  bool fact = true;
+  for (size_t j = 0; j < S && fact; ++j) {
+    const size_t i0 = (j == 0) ? 1 : 0;
+    const double* L = T + (i0 * S + j) * E;
+    for (size_t i = 0; i < S && fact; ++i)
+      if (i != j && i != i0 && memcmp(T + (i * S + j) * E, L, E * sizeof(double)) != 0) fact = false;
+    const double lo = L[0];
+    double hi = lo;
+    bool have_hi = false;
+    for (size_t e = 0; e < E && fact; ++e) {
+      const double v = L[e];
+      if (v == lo) continue;
+      if (!have_hi) { hi = v; have_hi = true; }
+      if (v != hi) { fact = false; break; }
+      d1[j * nwords + e / 64] |= 1ull << (e % 64);
+    }
+    elo[j] = exp(lo);
+    ehi[j] = exp(hi);
+  }
+  c.factored = fact;
+  c.fspad = nemo::factored_spad(c.S);
+  c.nwords = nwords;
+  if (c.d_U64) hipFree(c.d_U64);
+  c.d_U64 = nullptr;
+  HIPCHK(hipMalloc((void**)&c.d_U64, (S + 1) * E * 8));
+  HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
+  if (fact) {
+    if (c.d_D1w) hipFree(c.d_D1w);
+    if (c.d_elo) hipFree(c.d_elo);
+    if (c.d_ehi) hipFree(c.d_ehi);
+    HIPCHK(hipMalloc((void**)&c.d_D1w, d1.size() * 8));
+    HIPCHK(hipMalloc((void**)&c.d_elo, S * 8));
+    HIPCHK(hipMalloc((void**)&c.d_ehi, S * 8));
+    HIPCHK(hipMemcpy(c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
+  }
+  // grow the factored scratch if a batch was reserved before staging
+  if (c.cap_batch > 0) {
+    const int nb = c.cap_batch;
+    c.cap_batch = 0;
+    int rc2 = nemo_reserve(ctx, nb, 0);
+    if (rc2) return rc2;
+  }
   c.staged = true;
   return NEMO_OK;
+}
+
+static bool use_factored(const Ctx& c) {
+  if (c.score_path == 1) return false;
+  return c.factored;
 }
 
 // ---------------------------------------------------------------------------
@@ -230,6 +292,12 @@ int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double*
   if (batch > c.cap_batch) return fail(NEMO_ERR_STATE, "batch %d > reserved %d", batch, c.cap_batch);
   if (!d_pos || !d_w01 || !d_ll) return fail(NEMO_ERR_ARG, "null device pointer");
   hipStream_t st = pick(ctx, stream);
+  if (c.score_path == 2 && !c.factored)
+    return fail(NEMO_ERR_STATE, "score_path=2 (factored) but the staged table is not factorable");
+  if (use_factored(c)) {
+    HIPCHK(nemo::launch_score_factored(c, batch, cap, d_pos, d_w01, d_ll, d_cs, d_cells, d_ow, st));
+    return NEMO_OK;
+  }
   HIPCHK(nemo::launch_prep(c, batch, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
   HIPCHK(nemo::launch_score(c, batch, c.d_rows, c.d_sw, c.d_cnt, d_ll, d_cs, d_cells, d_ow, st));
   return NEMO_OK;
@@ -379,13 +447,20 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
   const int npairs = nemo::pairs_per_chain(c.S, cap);
   // eval #1 with order weights (nem_order_mcmc.py:181-182)
   HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, c.d_pairs, st));
-  HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll1, nullptr, nullptr, c.d_ow, st));
+  if (use_factored(c))
+    HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, d_w01, d_ll1, nullptr, nullptr, c.d_ow, st));
+  else
+    HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll1, nullptr, nullptr, c.d_ow, st));
   // every permissible pair's local optimum (nem_order_mcmc.py:186-189)
   HIPCHK(nemo::launch_local_opt_pairs(c, nchains, npairs, c.d_pairs, c.d_rows, d_w01, d_anc, c.d_ow,
                                       sig0, sig1, d_w_new, c.d_wdag, d_info, st));
   // eval #2 on the binarised weights (nem_order_mcmc.py:205-207)
-  HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, c.d_wdag, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
-  HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll_dag, nullptr, nullptr, nullptr, st));
+  if (use_factored(c)) {
+    HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, c.d_wdag, d_ll_dag, nullptr, nullptr, nullptr, st));
+  } else {
+    HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, c.d_wdag, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
+    HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll_dag, nullptr, nullptr, nullptr, st));
+  }
   c.ow_chains = nchains;
   return NEMO_OK;
 }
@@ -453,7 +528,24 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.xcd_remap = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "score_path") == 0) {
+    if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "score_path=%d not in {0,1,2}", value);
+    ctx->c.score_path = value;
+    return NEMO_OK;
+  }
   return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
+}
+
+int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!name || !value) return fail(NEMO_ERR_ARG, "null argument");
+  const Ctx& c = ctx->c;
+  if (strcmp(name, "xcd_remap") == 0) *value = c.xcd_remap;
+  else if (strcmp(name, "score_path") == 0) *value = c.score_path;
+  else if (strcmp(name, "factored") == 0) *value = c.factored ? 1 : 0;
+  else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
+  return NEMO_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,309 @@
+// nemo_factored.hip -- order score as a dense fp64 MFMA contraction.
+//
+// Every score table the reference builds (nem.py:36-47) has, for a parent
+// j != child i, T[i][j][e] = L[j][e] independent of i, and L[j][e] takes two
+// values (B where D[j][e] == 0, -A where D[j][e] == 1).  So each log factor of
+// compute_cell_ratios (nem_order_mcmc.py:83-86) is one of two numbers per
+// (i, j):  g_lo(i,j) = log(1 - w + w e^{lo_j}),  g_hi(i,j) = log(1 - w + w e^{hi_j}),
+// and the cell ratios become
+//     cell[i][e] = U[i][e] + G[i] + sum_j Delta[i][j] * D1[j][e],
+//     G[i] = sum_{j in pa(i)} g_lo(i,j),   Delta = g_hi - g_lo (0 off pa(i)),
+// a (S x S) . (S x E) product with K = S.  Staging detects the structure and
+// keeps D1 as a bit matrix; the product runs on v_mfma_f64_16x16x4_f64 and
+// the column log-sum-exp is fused into the epilogue.
+//
+// Children and parents are taken in ORDER position (pi), so Delta is strictly
+// lower triangular (a band of width `cap` with a parent cap) and the MFMA
+// k-loop of row block r stops at the diagonal: ~half the square's work.
+//
+// Geometry: one block = one evaluation x (WAVES*16) effects; each wave owns
+// 16 effects and ALL children (NR row blocks of 16), so the log-sum-exp over
+// children stays inside the wave (two xor-shuffles).  Delta is staged
+// through LDS per 64-parent chunk (row stride 66 doubles: conflict-free
+// ds_read_b64 A-fragments); the B fragments are bits of D1, expanded in
+// registers once per chunk.
+#include "nemo_internal.h"
+
+#include <math.h>
+
+namespace nemo {
+
+namespace {
+
+using f64x4 = __attribute__((ext_vector_type(4))) double;
+
+__device__ __forceinline__ double fwave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ int fxcd_work_index(int L, int N, int remap) {
+  if (!remap) return L;
+  const int x = L & 7, k = L >> 3;
+  const int q = N >> 3, r = N & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
+// ---------------------------------------------------------------------------
+// prep: Delta, G and pi of every evaluation.  grid = batch, block = 256.
+// Dp [b][SPAD][SPAD] (row = child position q, col = parent position p),
+// G  [b][SPAD], permo [b][SPAD] (node at position q; S for padding rows).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_factored_kernel(
+    int S, int SPAD, int cap, const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi, double* __restrict__ Dp,
+    double* __restrict__ G, int32_t* __restrict__ permo) {
+  __shared__ int perm[kMaxS];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  for (int k = tid; k < S; k += blockDim.x) perm[k] = 0;
+  __syncthreads();
+  for (int i = tid; i < S; i += blockDim.x) {
+    int pi = pos[(size_t)b * S + i];
+    pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);  // malformed input must not fault
+    perm[pi] = i;
+  }
+  __syncthreads();
+  for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
+  const int nw = blockDim.x / kWave;
+  for (int q = w; q < SPAD; q += nw) {
+    const int i = q < S ? perm[q] : 0;
+    const double* wrow = w01 + ((size_t)b * S + i) * S;
+    double* drow = Dp + ((size_t)b * SPAD + q) * SPAD;
+    double gsum = 0.0;
+    for (int p0 = 0; p0 < SPAD; p0 += kWave) {
+      const int p = p0 + lane;
+      double d = 0.0, glo = 0.0;
+      const bool ok = q < S && p < q && (cap == 0 || q - p <= cap);
+      if (ok) {
+        const int j = perm[p];
+        const double s = wrow[j];
+        const double lo = log(fma(s, e_lo[j] - 1.0, 1.0));
+        const double hi = log(fma(s, e_hi[j] - 1.0, 1.0));
+        d = hi - lo;
+        glo = lo;
+      }
+      if (p < SPAD) drow[p] = d;
+      gsum += fwave_sum(glo);
+    }
+    if (lane == 0) G[(size_t)b * SPAD + q] = gsum;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// score: grid = batch * ntiles (1-D, XCD remap, evaluation-major so the
+// blocks of one evaluation share its Delta in L2), block = WAVES waves.
+// ---------------------------------------------------------------------------
+template <int NR, int WAVES>
+__global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
+    int S, int E, int ntiles, int cap, const double* __restrict__ Dp,
+    const double* __restrict__ G, const int32_t* __restrict__ permo,
+    const uint64_t* __restrict__ D1w, int nwords, const double* __restrict__ U,
+    double* __restrict__ partial, double* __restrict__ cs_out, double* __restrict__ cells,
+    double* __restrict__ ow, int remap) {
+  constexpr int SPAD = NR * 16;
+  constexpr int KC = SPAD < 64 ? SPAD : 64;  // parents per LDS chunk
+  constexpr int LDA = KC + 2;                // padded row stride (doubles)
+  constexpr int NS = KC / 4;                 // k-steps per chunk
+  constexpr int COLS = WAVES * 16;
+  constexpr int WPR = (COLS + 63) / 64 + 1;  // D1 words per parent row a block can touch
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* A = lds;                                       // [SPAD][LDA]
+  uint64_t* words = (uint64_t*)(A + SPAD * LDA);         // [SPAD][WPR]
+  double* Gs = (double*)(words + SPAD * WPR);            // [SPAD]
+  int* perm_s = (int*)(Gs + SPAD);                       // [SPAD]
+
+  const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / ntiles;  // evaluation-major
+  const int tile = work - b * ntiles;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int e_blk = tile * COLS;
+  const int e_w0 = e_blk + w * 16;
+  const int col = lane & 15;
+  const int e = e_w0 + col;
+  const bool valid = e < E;
+  const int ec = valid ? e : E - 1;
+  const int word0 = e_blk >> 6;
+  const int shift = (e_w0 >> 6) - word0;  // which of the block's words this wave reads
+  const int bitpos = (e_w0 & 63) + col;
+
+  for (int k = tid; k < SPAD; k += blockDim.x) {
+    const int node = permo[(size_t)b * SPAD + k];
+    perm_s[k] = node;
+    Gs[k] = G[(size_t)b * SPAD + k];
+    for (int u = 0; u < WPR; ++u) {
+      const int wi = word0 + u;
+      words[k * WPR + u] = (node < S && wi < nwords) ? D1w[(size_t)node * nwords + wi] : 0ull;
+    }
+  }
+
+  f64x4 acc[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) acc[r] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+  const double* Db = Dp + (size_t)b * SPAD * SPAD;
+  for (int c0 = 0; c0 < SPAD; c0 += KC) {
+    __syncthreads();
+    // stage Delta[:, c0 .. c0+KC) (coalesced rows)
+    for (int k = tid; k < SPAD * KC; k += blockDim.x) {
+      const int row = k / KC, kk = k - row * KC;
+      A[row * LDA + kk] = Db[(size_t)row * SPAD + c0 + kk];
+    }
+    __syncthreads();
+    // B fragments of this chunk: lane holds D1[parent at 4s + lane/16][its effect]
+    double bf[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int p = c0 + 4 * s + (lane >> 4);
+      const uint64_t wd = words[p * WPR + shift];
+      bf[s] = (double)((wd >> bitpos) & 1ull);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      // parents of the rows of block r: positions < 16r+16 (and >= 16r-cap)
+      const int hi_step = (16 * r + 15 - c0) / 4;         // last k-step with p <= 16r+14
+      const int lo_pos = cap > 0 ? 16 * r - cap : 0;
+      const int lo_step = lo_pos > c0 ? (lo_pos - c0) / 4 : 0;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (s < lo_step || s > hi_step) continue;
+        const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
+        acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[s], acc[r], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: cells, column log-sum-exp, order weights --------------
+  // f64 16x16x4 C layout: col = lane & 15, row = (lane >> 4) + 4 * reg
+  double cell[NR][4];
+  double m = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int q = 16 * r + (lane >> 4) + 4 * g;
+      double v = -INFINITY;
+      if (q < S) v = U[(size_t)perm_s[q] * E + ec] + Gs[q] + acc[r][g];
+      cell[r][g] = v;
+      m = v > m ? v : m;
+    }
+  }
+  const double unull = U[(size_t)S * E + ec];
+  m = m > unull ? m : unull;
+  m = fmax(m, __shfl_xor(m, 16, kWave));
+  m = fmax(m, __shfl_xor(m, 32, kWave));
+  double l = 0.0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) l += exp(cell[r][g] - m);
+  l += __shfl_xor(l, 16, kWave);
+  l += __shfl_xor(l, 32, kWave);
+  l += exp(unull - m);
+  const double cs = m + log(l);
+  if (valid && lane < 16 && cs_out) cs_out[(size_t)b * E + e] = cs;
+  // per-wave partial over its 16 effects (lanes 0..15 hold one copy each)
+  double part = (valid && lane < 16) ? cs : 0.0;
+  part = fwave_sum(part);
+  const int ntw = ntiles * WAVES;
+  if (lane == 0) partial[(size_t)b * ntw + tile * WAVES + w] = part;
+  if ((cells || ow) && valid) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q = 16 * r + (lane >> 4) + 4 * g;
+        if (q < S) {
+          const size_t k = ((size_t)b * (S + 1) + perm_s[q]) * E + e;
+          if (cells) cells[k] = cell[r][g];
+          if (ow) ow[k] = exp(cell[r][g] - cs);
+        }
+      }
+    if (lane < 16) {
+      const size_t k = ((size_t)b * (S + 1) + S) * E + e;
+      if (cells) cells[k] = unull;
+      if (ow) ow[k] = exp(unull - cs);
+    }
+  }
+}
+
+__global__ void finalize_factored_kernel(int batch, int n, const double* __restrict__ partial,
+                                         double* __restrict__ ll) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double s = 0.0;
+  for (int t = 0; t < n; ++t) s += partial[(size_t)b * n + t];
+  ll[b] = s;
+}
+
+template <int NR>
+hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_ll, double* d_cs, double* d_cells,
+                         double* d_ow, hipStream_t st) {
+  constexpr int WAVES = kFactWaves;
+  constexpr int SPAD = NR * 16;
+  constexpr int KC = SPAD < 64 ? SPAD : 64;
+  constexpr int COLS = WAVES * 16;
+  constexpr int WPR = (COLS + 63) / 64 + 1;
+  const int nt = (c.E + COLS - 1) / COLS;
+  const size_t lds = (size_t)SPAD * (KC + 2) * 8 + (size_t)SPAD * WPR * 8 + SPAD * 8 + SPAD * 4;
+  score_factored_kernel<NR, WAVES><<<dim3(nt * batch), WAVES * kWave, lds, st>>>(
+      c.S, c.E, nt, cap, c.d_fDp, c.d_fG, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
+      c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  return hipSuccess;
+}
+
+}  // namespace
+
+int factored_spad(int S) {
+  const int nr = (S + 15) / 16;
+  const int sizes[] = {1, 2, 4, 8, 16};
+  for (int v : sizes)
+    if (nr <= v) return v * 16;
+  return -1;
+}
+
+int factored_partials(const Ctx& c) {
+  const int cols = kFactWaves * 16;
+  return ((c.E + cols - 1) / cols) * kFactWaves;
+}
+
+hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
+                                 const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
+                                 double* d_ow, hipStream_t st) {
+  const int spad = c.fspad;
+  prep_factored_kernel<<<batch, 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo, c.d_ehi,
+                                              c.d_fDp, c.d_fG, c.d_fperm);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+    e0 = c.ev_pool[c.ev_used++];
+    e1 = c.ev_pool[c.ev_used++];
+    hipEventRecord(e0, st);
+  }
+  switch (spad / 16) {
+    case 1: err = launch_fact_t<1>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+    case 2: err = launch_fact_t<2>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+    case 4: err = launch_fact_t<4>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+    case 8: err = launch_fact_t<8>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+    case 16: err = launch_fact_t<16>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  if (err != hipSuccess) return err;
+  if (e1) {
+    (void)hipEventRecord(e1, st);
+    c.launches++;
+  }
+  const int np = factored_partials(c);
+  finalize_factored_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, np, c.d_fpartial, d_ll);
+  return hipGetLastError();
+}
+
+}  // namespace nemo

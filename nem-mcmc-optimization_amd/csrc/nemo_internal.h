@@ -15,6 +15,7 @@ constexpr int kWave = 64;
 constexpr int kMaxS = 256;         // one prep block covers all S-genes
 constexpr int kScoreWaves = 4;     // waves per score block (child split)
 constexpr int kTileCols = kWave;   // effects per score block
+constexpr int kFactWaves = 8;      // waves per factored-score block (16 effects each)
 
 // Device state of one staged model on one GPU.
 struct Ctx {
@@ -47,6 +48,21 @@ struct Ctx {
   double* d_c = nullptr;           // generic local-opt inputs [n][E] (grown on demand)
   size_t c_capacity = 0;
   int ow_chains = 0;               // chains whose order weights d_ow holds
+
+  // factored (MFMA) path: available when every off-diagonal table row is
+  // shared by all children and two-valued (all tables nem.py builds)
+  int score_path = 0;              // option "score_path": 0 auto, 1 stream, 2 factored
+  bool factored = false;
+  int fspad = 0;                   // S rounded up to the MFMA row-block size
+  int nwords = 0;                  // 64-bit words per D1 row
+  uint64_t* d_D1w = nullptr;       // [S][nwords] bit D1[j][e]: T row j takes its "hi" value
+  double* d_elo = nullptr;         // [S] exp(lo_j)
+  double* d_ehi = nullptr;         // [S] exp(hi_j)
+  double* d_U64 = nullptr;         // U in fp64 [S+1][E]
+  double* d_fDp = nullptr;         // [cap][fspad][fspad] Delta in order positions
+  double* d_fG = nullptr;          // [cap][fspad]
+  int32_t* d_fperm = nullptr;      // [cap][fspad]
+  double* d_fpartial = nullptr;    // [cap][factored_partials]
 
   // grouped (reuse) evaluation scratch
   int cap_group_batch = 0;
@@ -87,5 +103,12 @@ hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const doub
 
 // number of (child, parent) pairs per chain for a given cap
 int pairs_per_chain(int S, int cap);
+
+// factored MFMA path (nemo_factored.hip)
+int factored_spad(int S);
+int factored_partials(const Ctx& c);
+hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
+                                 const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
+                                 double* d_ow, hipStream_t st);
 
 }  // namespace nemo

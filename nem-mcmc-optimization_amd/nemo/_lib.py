@@ -44,6 +44,7 @@ SIGNATURES = [
                                             C.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("nemo_fetch_order_weights", C.c_int, [_vp, C.c_int, _f64p]),
     ("nemo_set_option", C.c_int, [_vp, C.c_char_p, C.c_int]),
+    ("nemo_get_option", C.c_int, [_vp, C.c_char_p, _i32p]),
     ("nemo_timing_enable", C.c_int, [_vp, C.c_int]),
     ("nemo_timing_read", C.c_int, [_vp, _f64p, _i32p]),
 ]

@@ -145,6 +145,16 @@ class Engine:
     def set_option(self, name: str, value: int):
         check(_lib.load().nemo_set_option(self._ctx, name.encode(), int(value)))
 
+    def get_option(self, name: str) -> int:
+        v = C.c_int32(0)
+        check(_lib.load().nemo_get_option(self._ctx, name.encode(), C.byref(v)))
+        return v.value
+
+    @property
+    def factored(self) -> bool:
+        """True when the staged table has the NEM structure the MFMA kernel uses."""
+        return bool(self.get_option("factored"))
+
     # -- timing of the score kernel ------------------------------------------
     def timing(self, enable: bool):
         check(_lib.load().nemo_timing_enable(self._ctx, 1 if enable else 0))

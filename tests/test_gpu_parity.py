@@ -264,3 +264,47 @@ def test_chain_batch_equals_single_chains():
         assert np.array_equal(np.array(single.accepted), cb.accepted[:, k])
         assert b == best[k]
         assert np.array_equal(single.best_order, best_orders[k])
+
+
+@pytest.mark.parametrize("name,s,e,cap", [("net2", 11, 184, 0), ("C2", 16, 500, 0), ("C3", 64, 2000, 0),
+                                          ("C5cap", 128, 5000, 6)])
+def test_factored_mfma_path_vs_golden_and_stream(name, s, e, cap):
+    """The factored MFMA kernel (score_path=2) against the reference goldens
+    and against the streaming kernel (score_path=1) on the same inputs."""
+    z = golden(f"eval_{name}.npz")
+    if name == "net2":
+        t = golden("net2_tables.npz")
+        eng = Engine(t["U"], t["T"])
+    else:
+        m = generator.synthetic_nem(s, e, 0)
+        eng = Engine(m.U, m.get_score_tensor())
+    assert eng.factored
+    pos, w01 = _golden_batch(z)
+    eng.set_option("score_path", 2)
+    f = eng.score(pos, w01, cap=cap, want_cs=True, want_cells=True, want_ow=True)
+    eng.set_option("score_path", 1)
+    st = eng.score(pos, w01, cap=cap, want_cs=True, want_cells=True, want_ow=True)
+    assert np.max(np.abs(f["ll"] - z["ll"])) <= LL_TOL
+    assert np.max(np.abs(f["cs"] - z["cs"])) <= 1e-9
+    assert np.max(np.abs(f["cells"] - st["cells"])) <= 1e-10
+    assert np.max(np.abs(f["ow"] - st["ow"])) <= 1e-12
+    if "ow0" in z.files:
+        assert np.max(np.abs(f["ow"][0] - z["ow0"])) <= 1e-11
+    eng.close()
+
+
+def test_factored_detection_rejects_generic_tables():
+    rng = np.random.default_rng(8)
+    s, e = 6, 70
+    t = rng.normal(0, 1, (s, s, e))
+    u = rng.normal(-5, 1, (s + 1, e))
+    eng = Engine(u, t)
+    assert not eng.factored
+    eng.set_option("score_path", 2)
+    with pytest.raises(RuntimeError, match="not factorable"):
+        eng.score(np.arange(s, dtype=np.int32)[None], np.full((1, s, s), 0.5))
+    eng.set_option("score_path", 0)  # auto -> stream
+    perm = rng.permutation(s)
+    w01 = rng.random((s, s))
+    ll = eng.score(_pos(perm)[None], w01[None])[0]
+    assert abs(ll - no.order_score(u, t, perm, w01)) <= 1e-9

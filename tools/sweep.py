@@ -38,9 +38,11 @@ def main():
         eng = Engine.for_nem(m, dtype=dtype)
         variants = []
         for batch in (32, 128, 512):
-            for group in ((1, 4, 8, 16) if cap == 0 else (1,)):
+            for group in ((1, 4, 8) if cap == 0 else (1,)):
                 for remap in (0, 1):
-                    variants.append((batch, group, remap))
+                    variants.append((batch, group, remap, 1))
+            variants.append((batch, 1, 1, 2))   # factored MFMA path
+            variants.append((batch, 1, 0, 2))
         maxb = max(v[0] for v in variants)
         eng.reserve(maxb)
         rng = np.random.default_rng(5)
@@ -51,14 +53,16 @@ def main():
         with torch.cuda.stream(stream):
             st = stream.cuda_stream
             for v in variants:  # warm-up / first-use allocations
-                batch, group, remap = v
+                batch, group, remap, path = v
                 eng.set_option("xcd_remap", remap)
+                eng.set_option("score_path", path)
                 eng.score_dev(batch, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(), cap=cap, stream=st, group=group)
             torch.cuda.synchronize()
             for _ in range(args.rounds):
                 for v in variants:
-                    batch, group, remap = v
+                    batch, group, remap, path = v
                     eng.set_option("xcd_remap", remap)
+                    eng.set_option("score_path", path)
                     eng.timing(True)
                     for _ in range(args.steps):
                         eng.score_dev(batch, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(), cap=cap,
@@ -68,11 +72,13 @@ def main():
                     eng.timing(False)
                     times[v].append(ms / n)
         for v, ts in times.items():
-            batch, group, remap = v
+            batch, group, remap, path = v
             med = float(np.median(ts))
-            results[f"{cfg} b={batch} g={group} remap={remap}"] = {
+            results[f"{cfg} b={batch} g={group} remap={remap} path={'factored' if path == 2 else 'stream'}"] = {
                 "median_ms": med, "min_ms": float(np.min(ts)),
                 "evals_per_s_kernel": batch / (med / 1e3)}
+        eng.set_option("score_path", 0)
+        eng.set_option("xcd_remap", 1)
         # fused per-step scorer (eval #1 + local optima + eval #2)
         from nemo.nem_order_mcmc import SIG0, SIG1
         for nch in (1, 16):
