@@ -147,9 +147,13 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
   for (int r = 0; r < NR; ++r) acc[r] = f64x4{0.0, 0.0, 0.0, 0.0};
 
   const double* Db = Dp + (size_t)b * SPAD * SPAD;
-  for (int c0 = 0; c0 < SPAD; c0 += KC) {
+  constexpr int NCH = SPAD / KC;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int c0 = c * KC;
     __syncthreads();
-    // stage Delta[:, c0 .. c0+KC) (coalesced rows)
+    // stage Delta[:, c0 .. c0+KC) (coalesced rows); only rows that have
+    // parents in this chunk (row q needs p < q, i.e. q > c0)
     for (int k = tid; k < SPAD * KC; k += blockDim.x) {
       const int row = k / KC, kk = k - row * KC;
       A[row * LDA + kk] = Db[(size_t)row * SPAD + c0 + kk];
@@ -163,17 +167,17 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
       const uint64_t wd = words[p * WPR + shift];
       bf[s] = (double)((wd >> bitpos) & 1ull);
     }
+    // lower-triangular k-loop, fully static: row block r (positions
+    // 16r..16r+15) has parents only at positions <= 16r+14.  k-steps outer,
+    // row blocks inner, so consecutive MFMAs use independent accumulators.
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      // parents of the rows of block r: positions < 16r+16 (and >= 16r-cap)
-      const int hi_step = (16 * r + 15 - c0) / 4;         // last k-step with p <= 16r+14
-      const int lo_pos = cap > 0 ? 16 * r - cap : 0;
-      const int lo_step = lo_pos > c0 ? (lo_pos - c0) / 4 : 0;
+    for (int s = 0; s < NS; ++s) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if (s < lo_step || s > hi_step) continue;
-        const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
-        acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[s], acc[r], 0, 0, 0);
+      for (int r = 0; r < NR; ++r) {
+        if (c0 + 4 * s <= 16 * r + 14) {
+          const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
+          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[s], acc[r], 0, 0, 0);
+        }
       }
     }
   }
