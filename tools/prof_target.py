@@ -22,6 +22,7 @@ def main():
         S, E, seed, cap, dtype = generator.CONFIGS[cfg]
         m = generator.config_nem(cfg)
         eng = Engine.for_nem(m, dtype=dtype)
+        eng.set_option("score_path", int(os.environ.get("NEMO_PROF_PATH", "0")))
         eng.reserve(B)
         rng = np.random.default_rng(5)
         pos = torch.from_numpy(np.array([rng.permutation(S) for _ in range(B)], dtype=np.int32)).cuda()
