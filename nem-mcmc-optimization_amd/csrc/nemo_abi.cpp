@@ -528,6 +528,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.xcd_remap = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "fact_resident") == 0) {
+    ctx->c.fact_resident = value < 0 ? 0 : value;  // 0 off; 1, 2, 4: min waves/SIMD
+    return NEMO_OK;
+  }
   if (strcmp(name, "score_path") == 0) {
     if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "score_path=%d not in {0,1,2}", value);
     ctx->c.score_path = value;
@@ -544,6 +548,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   if (strcmp(name, "xcd_remap") == 0) *value = c.xcd_remap;
   else if (strcmp(name, "score_path") == 0) *value = c.score_path;
   else if (strcmp(name, "factored") == 0) *value = c.factored ? 1 : 0;
+  else if (strcmp(name, "fact_resident") == 0) *value = c.fact_resident;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;
 }

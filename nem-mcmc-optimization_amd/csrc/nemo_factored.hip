@@ -259,6 +259,164 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// resident variant (S <= 64): a block stages its evaluation's Delta, G, pi
+// and the D1 bits of its column range ONCE, then every wave walks its share
+// of 16-effect tiles with no further barrier.  Per tile the epilogue's U rows
+// are requested before the MFMA phase, so their latency hides under it.
+// grid = batch * split (split column ranges per evaluation), block = WAVES.
+// ---------------------------------------------------------------------------
+template <int NR, int WAVES, int MINW>
+__global__ __launch_bounds__(WAVES * kWave, MINW) void score_factored_resident_kernel(
+    int S, int E, int ntiles, int split, const double* __restrict__ Dp,
+    const double* __restrict__ G, const int32_t* __restrict__ permo,
+    const uint64_t* __restrict__ D1w, int nwords, const double* __restrict__ U,
+    double* __restrict__ partial, double* __restrict__ cs_out, double* __restrict__ cells,
+    double* __restrict__ ow, int remap) {
+  constexpr int SPAD = NR * 16;
+  constexpr int LDA = SPAD + 1;
+  constexpr int NS = SPAD / 4;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tiles_per = (ntiles + split - 1) / split;     // 16-effect tiles per block
+  const int wpb = (tiles_per * 16 + 63) / 64 + 1;         // D1 words per row in the range
+  double* A = lds;                                        // [SPAD][LDA]
+  double* Gs = A + SPAD * LDA;                            // [SPAD]
+  double* etab = Gs + SPAD;                               // [64]
+  uint64_t* words = (uint64_t*)(etab + 64);               // [SPAD][wpb]
+  int* perm_s = (int*)(words + SPAD * wpb);               // [SPAD]
+
+  const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / split;
+  const int part_id = work - b * split;
+  const int t_begin = part_id * tiles_per;
+  const int t_end = min(ntiles, t_begin + tiles_per);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int word0 = (t_begin * 16) >> 6;
+
+  if (tid < 64) etab[tid] = exp2((double)tid * (1.0 / 64.0));
+  for (int k = tid; k < SPAD; k += blockDim.x) {
+    const int node = permo[(size_t)b * SPAD + k];
+    perm_s[k] = node;
+    Gs[k] = G[(size_t)b * SPAD + k];
+    for (int u = 0; u < wpb; ++u) {
+      const int wi = word0 + u;
+      words[k * wpb + u] = (node < S && wi < nwords) ? D1w[(size_t)node * nwords + wi] : 0ull;
+    }
+  }
+  const double* Db = Dp + (size_t)b * SPAD * SPAD;
+  for (int k = tid; k < SPAD * SPAD; k += blockDim.x) {
+    const int row = k / SPAD, kk = k - row * SPAD;
+    if (kk <= (row | 15)) A[row * LDA + kk] = Db[k];
+  }
+  __syncthreads();
+
+  const int col = lane & 15;
+  for (int t = t_begin + w; t < t_end; t += WAVES) {
+    const int e_w0 = t * 16;
+    const int e = e_w0 + col;
+    const bool valid = e < E;
+    const int ec = valid ? e : E - 1;
+    // epilogue operands first: their latency hides under the MFMAs
+    double u[NR][4];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q = 16 * r + (lane >> 4) + 4 * g;
+        u[r][g] = (q < S) ? U[(size_t)perm_s[q] * E + ec] : 0.0;
+      }
+    const double unull = U[(size_t)S * E + ec];
+    const int widx = (e_w0 >> 6) - word0;
+    const int bitpos = (e_w0 & 63) + col;
+    f64x4 acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int p = 4 * s + (lane >> 4);
+      const double bf = (double)((words[p * wpb + widx] >> bitpos) & 1ull);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        if (4 * s <= 16 * r + 14) {
+          const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
+          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf, acc[r], 0, 0, 0);
+        }
+      }
+    }
+    double m = unull;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q = 16 * r + (lane >> 4) + 4 * g;
+        const double v = (q < S) ? u[r][g] + Gs[q] + acc[r][g] : -INFINITY;
+        u[r][g] = v;  // now the cell
+        m = v > m ? v : m;
+      }
+    m = fmax(m, __shfl_xor(m, 16, kWave));
+    m = fmax(m, __shfl_xor(m, 32, kWave));
+    double l = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) l += exp_tab(u[r][g] - m, etab);
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
+    l += exp_tab(unull - m, etab);
+    const double cs = m + log(l);
+    if (valid && lane < 16 && cs_out) cs_out[(size_t)b * E + e] = cs;
+    double part = (valid && lane < 16) ? cs : 0.0;
+    part = fwave_sum(part);
+    if (lane == 0) partial[(size_t)b * ntiles + t] = part;
+    if ((cells || ow) && valid) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int q = 16 * r + (lane >> 4) + 4 * g;
+          if (q < S) {
+            const size_t k = ((size_t)b * (S + 1) + perm_s[q]) * E + e;
+            if (cells) cells[k] = u[r][g];
+            if (ow) ow[k] = exp_tab(u[r][g] - cs, etab);
+          }
+        }
+      if (lane < 16) {
+        const size_t k = ((size_t)b * (S + 1) + S) * E + e;
+        if (cells) cells[k] = unull;
+        if (ow) ow[k] = exp_tab(unull - cs, etab);
+      }
+    }
+  }
+}
+
+template <int NR>
+hipError_t launch_fact_resident_t(Ctx& c, int batch, double* d_cs, double* d_cells, double* d_ow,
+                                  hipStream_t st) {
+  constexpr int WAVES = kFactWaves;
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  // enough blocks to cover the CUs twice, each owning whole waves of tiles
+  int split = (2 * 256 + batch - 1) / batch;
+  const int max_split = (ntiles + WAVES - 1) / WAVES;
+  split = split < 1 ? 1 : (split > max_split ? max_split : split);
+  const int tiles_per = (ntiles + split - 1) / split;
+  const int wpb = (tiles_per * 16 + 63) / 64 + 1;
+  const size_t lds = (size_t)SPAD * (SPAD + 1) * 8 + SPAD * 8 + 64 * 8 + (size_t)SPAD * wpb * 8 +
+                     SPAD * 4;
+#define NEMO_FR(MINW)                                                                         \
+  score_factored_resident_kernel<NR, WAVES, MINW><<<dim3(batch * split), WAVES * kWave, lds, st>>>( \
+      c.S, c.E, ntiles, split, c.d_fDp, c.d_fG, c.d_fperm, c.d_D1w, c.nwords,                 \
+      (const double*)c.d_U64, c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap)
+  // option fact_resident = minimum waves per SIMD the register budget targets
+  if (c.fact_resident >= 4) NEMO_FR(4);
+  else if (c.fact_resident >= 2) NEMO_FR(2);
+  else NEMO_FR(1);
+#undef NEMO_FR
+  return hipGetLastError();
+}
+
 __global__ void finalize_factored_kernel(int batch, int n, const double* __restrict__ partial,
                                          double* __restrict__ ll) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -316,20 +474,32 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     e1 = c.ev_pool[c.ev_used++];
     hipEventRecord(e0, st);
   }
-  switch (spad / 16) {
-    case 1: err = launch_fact_t<1>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-    case 2: err = launch_fact_t<2>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-    case 4: err = launch_fact_t<4>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-    case 8: err = launch_fact_t<8>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-    case 16: err = launch_fact_t<16>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-    default: return hipErrorInvalidValue;
+  const bool resident = c.fact_resident && spad <= 64;
+  if (resident) {
+    switch (spad / 16) {
+      case 1: err = launch_fact_resident_t<1>(c, batch, d_cs, d_cells, d_ow, st); break;
+      case 2: err = launch_fact_resident_t<2>(c, batch, d_cs, d_cells, d_ow, st); break;
+      case 4: err = launch_fact_resident_t<4>(c, batch, d_cs, d_cells, d_ow, st); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (spad / 16) {
+      case 1: err = launch_fact_t<1>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      case 2: err = launch_fact_t<2>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      case 4: err = launch_fact_t<4>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      case 8: err = launch_fact_t<8>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      case 16: err = launch_fact_t<16>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      default: return hipErrorInvalidValue;
+    }
   }
   if (err != hipSuccess) return err;
   if (e1) {
     (void)hipEventRecord(e1, st);
     c.launches++;
   }
-  const int np = factored_partials(c);
+  // per-evaluation partials: one per 16-effect tile (resident) or per wave
+  // slot of the 128-effect blocks (chunked); summed in a fixed order
+  const int np = resident ? (c.E + 15) / 16 : factored_partials(c);
   finalize_factored_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, np, c.d_fpartial, d_ll);
   return hipGetLastError();
 }
