@@ -1,15 +1,17 @@
 """Benchmark: order-score evaluations/s on the synthetic 64 S-gene x 2000
 effect NEM (BASELINE.json metric, config C3; C4 = the same per GPU at N > 1).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--group G]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--path auto|stream|factored]
 
 A step is one batched pass of the hot path over B (pos, W) evaluations whose
-inputs are already resident in HBM: prep (parent lists) + score kernel +
-finalize, enqueued on torch's current stream through the C-ABI.  With N > 1
-(torchrun, one rank per GPU) every rank evaluates its own B evaluations of
-its own chains (weak scaling, no data-path collective); the only collective
-is one RCCL all-gather of per-chain best scores at the end of the timed
-region (C4).  Rank 0 prints one JSON line.
+inputs are already resident in HBM, enqueued on one HIP stream through the
+C-ABI: for the default path (the staged C3 table has the NEM structure, so
+the factored kernel is selected) that is prep (Delta in order positions) +
+the fp64-MFMA score kernel with fused log-sum-exp + a fixed-order finalize.
+With N > 1 (torchrun, one rank per GPU) every rank evaluates its own B
+evaluations (weak scaling, no data-path collective); the only collective is
+one RCCL all-gather of per-chain best scores at the end of the timed region
+(C4).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -24,18 +26,30 @@ sys.path.insert(0, os.path.join(HERE, "nem-mcmc-optimization_amd"))
 
 import numpy as np  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F64_MFMA_PEAK_TF = 78.6  # v_mfma_f64_16x16x4_f64: 2048 FLOP / 64 busy cycles / SIMD (PMC-checked)
+PATHS = {"auto": 0, "stream": 1, "factored": 2}
+
+
+def n_pairs(S, cap):
+    return sum(min(q, cap) if cap else q for q in range(S))
 
 
 def algorithmic_bytes_per_eval(S, E, cap, b):
     """P*E*b (table rows) + (S+1)*E*b (U) + S^2*b (W) + 4S (pos) + b (ll)."""
-    P = sum(min(q, cap) if cap else q for q in range(S))
-    return P * E * b + (S + 1) * E * b + S * S * b + 4 * S + b
+    return n_pairs(S, cap) * E * b + (S + 1) * E * b + S * S * b + 4 * S + b
+
+
+def algorithmic_flops_per_eval(S, E, cap):
+    """Factored form: cell = U + G + Delta.D1 over the permissible (i, j):
+    2 FLOP per (pair, effect)."""
+    return 2 * n_pairs(S, cap) * E
 
 
 def cpu_baseline(m, seconds=10.0):
     """The oracle (numpy restatement of the reference's compute_cell_ratios +
-    calculate_ll, nem_order_mcmc.py:79-93) timed on this host, 1 thread."""
+    calculate_ll, nem_order_mcmc.py:79-93, same operation order) timed on
+    this host, one thread."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import nemo_oracle as no
     from scipy.special import expit
@@ -50,17 +64,45 @@ def cpu_baseline(m, seconds=10.0):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{n} order-score evals of the 64x2000 C3 model in {dt:.1f} s, "
-                      "oracle numpy loop form (reference operation order), OMP_NUM_THREADS=1"}
+            "sample": f"{n} order-score evals of the 64x2000 C3 model in {dt:.1f} s: oracle numpy "
+                      "loop form (reference operation order), one thread, this host"}
 
 
-def load_traffic(workload):
+def load_traffic(key):
     p = os.path.join(HERE, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None
     with open(p) as fh:
-        d = json.load(fh)
-    return d.get(workload)
+        return json.load(fh).get(key)
+
+
+def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, world, dist):
+    def step():
+        eng.score_dev(B, d_pos.data_ptr(), d_w01.data_ptr(), d_ll.data_ptr(), cap=cap, stream=stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if world > 1:
+        # C4: gather every rank's per-chain best score (tiny, latency-bound)
+        best = d_ll.max().reshape(1)
+        allb = [torch.empty_like(best) for _ in range(world)]
+        dist.all_gather(allb, best)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms, launches = eng.timing_read()
+    eng.timing(False)
+    return wall, kern_ms / max(launches, 1)
 
 
 def main():
@@ -68,10 +110,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("NEMO_BENCH_BATCH", 128)))
-    ap.add_argument("--group", type=int, default=int(os.environ.get("NEMO_BENCH_GROUP", 1)))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("NEMO_BENCH_BATCH", 512)))
+    ap.add_argument("--path", default=os.environ.get("NEMO_BENCH_PATH", "auto"), choices=list(PATHS))
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the stream-kernel and MCMC lines")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
@@ -93,6 +136,8 @@ def main():
     S, E, seed, cap, dtype = generator.CONFIGS[args.config]
     m = generator.config_nem(args.config)
     eng = Engine.for_nem(m, device=local, dtype=dtype)
+    eng.set_option("score_path", PATHS[args.path])
+    factored = eng.factored and args.path != "stream"
     B = args.batch
     eng.reserve(B)
     rng = np.random.default_rng(1000 + rank)
@@ -105,51 +150,67 @@ def main():
     torch.cuda.set_stream(side)
     stream = side.cuda_stream
 
-    def step():
-        eng.score_dev(B, d_pos.data_ptr(), d_w01.data_ptr(), d_ll.data_ptr(), cap=cap,
-                      stream=stream, group=args.group)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    eng.timing(True)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(side)
-    for _ in range(args.steps):
-        step()
-    if world > 1:
-        # C4: gather every chain's best score (tiny, latency-bound)
-        best = d_ll.max().reshape(1)
-        allb = [torch.empty_like(best) for _ in range(world)]
-        dist.all_gather(allb, best)
-    ev1.record(side)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms, launches = eng.timing_read()
-    eng.timing(False)
+    wall, kern_ms = timed_steps(eng, torch, B, cap, args.steps, args.warmup, d_pos, d_w01, d_ll,
+                                stream, world, dist)
     t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     t_max = float(t_max.item())
-
-    # parity spot check of the timed results (outside the timed region)
     ll = d_ll.cpu().numpy()
-    sys.path.insert(0, os.path.join(HERE, "oracle"))
+
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        # the generic streaming kernel on the same model (HBM-priced roofline)
+        eng.set_option("score_path", 1)
+        Bs = min(B, 128)
+        w_s, k_s = timed_steps(eng, torch, Bs, cap, 10, 2, d_pos, d_w01, d_ll, stream, 1, dist)
+        bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
+        ach = Bs * bpe / (k_s / 1e3) / 1e9
+        extras["stream_kernel"] = {
+            "evals_per_s": Bs * 10 / w_s, "batch": Bs, "kernel_avg_ms": k_s,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "bytes_per_eval": bpe,
+                         "traffic": load_traffic(f"{args.config}:stream:b{Bs}"),
+                         "note": "the 65.5 MB exp(T) table is Infinity-Cache resident at C3, so "
+                                 "algorithmic bytes exceed HBM bytes (traffic = PMC bytes)"}}
+        eng.set_option("score_path", PATHS[args.path])
+        # fused per-step scorer of the sampler: 16 chains (C4 share of one GPU)
+        from nemo.nem_order_mcmc import SIG0, SIG1
+        nch = 16
+        pos_h = pos[:nch]
+        w_h = rng.uniform(-3, 3, (nch, S, S))
+        anc = np.clip(rng.random((nch, S, S)) - 0.5, 0, 1)
+        eng.optimal_weights(pos_h, expit(w_h), anc, w_h, SIG0, SIG1, cap=cap, raise_on_fail=False)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            eng.optimal_weights(pos_h, expit(w_h), anc, w_h, SIG0, SIG1, cap=cap, raise_on_fail=False)
+            ts.append(time.perf_counter() - t0)
+        fs = float(np.median(ts))
+        extras["mcmc_fused_step"] = {
+            "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
+            "includes": "H2D of pos/W/anc, eval#1 with order weights, 2016 L-BFGS-B local optima "
+                        "per chain, eval#2 on binarised weights, D2H"}
 
     if rank == 0:
-        b = 8 if dtype == "f64" else 4
-        bpe = algorithmic_bytes_per_eval(S, E, cap, b)
-        avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
-        achieved = B * bpe / avg_kernel_s / 1e9
-        workload = f"{args.config} synthetic S={S} E={E} cap={cap} {dtype}, batch={B}, group={args.group}"
+        if factored:
+            fpe = algorithmic_flops_per_eval(S, E, cap)
+            ach = B * fpe / (kern_ms / 1e3) / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                    "frac": ach / F64_MFMA_PEAK_TF,
+                    "traffic": load_traffic(f"{args.config}:factored:b{B}"),
+                    "kernel": "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)",
+                    "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
+                    "note": "FLOPs of the dense contraction Delta.D1 over the permissible pairs; "
+                            "the fused log-sum-exp epilogue (S+1)*E exps/eval is VALU work on top"}
+        else:
+            bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
+            ach = B * bpe / (kern_ms / 1e3) / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(f"{args.config}:stream:b{B}"),
+                    "kernel": "score_kernel (streams exp(T) rows)", "kernel_avg_ms": kern_ms,
+                    "bytes_per_eval": bpe}
+        path = "factored" if factored else "stream"
         rec = {
             "metric": "order-score evals/sec (64 S-genes x 2000 effects); HBM GB/s fraction",
             "value": world * B * args.steps / t_max,
@@ -162,24 +223,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64" if dtype == "f64" else "f32",
-            "data": "synthetic (build-defined generator, SURVEY.md 8(d)); random orders and W~U(-3,3)",
-            "config": {"workload": workload, "S": S, "E": E, "cap": cap, "batch_per_gpu": B,
-                       "group": args.group, "evals_per_step": world * B,
-                       "parallelism": f"chains sharded, {world} GPU(s), RCCL all-gather of best scores"},
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(f"{args.config}:b{B}:g{args.group}"),
-                "kernel": "score_kernel" if args.group == 1 else "score_group_kernel",
-                "kernel_avg_ms": avg_kernel_s * 1e3,
-                "bytes_per_eval": bpe,
-            },
-            "wall_check_ms_per_step": 1e3 * ev0.elapsed_time(ev1) / args.steps,
+            "data": "synthetic (build-defined generator, SURVEY.md 8(d)); random orders, W~U(-3,3)",
+            "config": {"workload": f"{args.config}: S={S} E={E} cap={cap} {dtype}, {B} order-score "
+                                   f"evaluations per step per GPU, {path} kernel",
+                       "S": S, "E": E, "cap": cap, "batch_per_gpu": B, "path": path,
+                       "parallelism": f"independent evaluations/chains sharded over {world} GPU(s); "
+                                      "one RCCL all-gather of best scores"},
+            "roofline": roof,
             "ll_sample": float(ll[0]),
         }
+        rec.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(m, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

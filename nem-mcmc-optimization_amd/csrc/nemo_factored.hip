@@ -75,7 +75,10 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
     const double* __restrict__ e_lo, const double* __restrict__ e_hi, double* __restrict__ Dp,
     double* __restrict__ G, int32_t* __restrict__ permo) {
   __shared__ int perm[kMaxS];
-  const int b = blockIdx.x;
+  // block = (evaluation, group of 16 child positions); 4 waves x 4 rows
+  const int ngroups = SPAD / 16;
+  const int b = blockIdx.x / ngroups;
+  const int grp = blockIdx.x - b * ngroups;
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -87,9 +90,10 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
     perm[pi] = i;
   }
   __syncthreads();
-  for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
+  if (grp == 0)
+    for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
   const int nw = blockDim.x / kWave;
-  for (int q = w; q < SPAD; q += nw) {
+  for (int q = 16 * grp + w; q < 16 * grp + 16; q += nw) {
     const int i = q < S ? perm[q] : 0;
     const double* wrow = w01 + ((size_t)b * S + i) * S;
     double* drow = Dp + ((size_t)b * SPAD + q) * SPAD;
@@ -464,7 +468,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st) {
   const int spad = c.fspad;
-  prep_factored_kernel<<<batch, 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo, c.d_ehi,
+  prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo, c.d_ehi,
                                               c.d_fDp, c.d_fG, c.d_fperm);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;

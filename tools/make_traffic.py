@@ -1,0 +1,44 @@
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/traffic.json:
+HBM-side bytes per launch of the score kernels, corrected as
+MI355X_MICROARCH.md prescribes (FETCH_SIZE reads 1/2 of a wide streaming read
+on gfx950 -> x2; both counters in KiB -> x1024).
+
+    python tools/make_traffic.py <fetch_csv> <write_csv> <key_prefix> [profiles/traffic.json]
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        if "score_factored_kernel" in name:
+            agg["factored"].append(float(r["Counter_Value"]))
+        elif "score_kernel" in name:
+            agg["stream"].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    fetch, write, prefix = sys.argv[1:4]
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(__file__), "..", "profiles", "traffic.json")
+    f = per_kernel(fetch, "FETCH_SIZE")
+    w = per_kernel(write, "WRITE_SIZE")
+    data = json.load(open(out)) if os.path.exists(out) else {}
+    for kind in f:
+        key = prefix.replace("{kind}", kind)
+        data[key] = {"bytes_per_launch": 2 * 1024 * f[kind] + 1024 * w.get(kind, 0.0),
+                     "fetch_size_kib": f[kind], "write_size_kib": w.get(kind, 0.0),
+                     "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE, KiB"}
+    json.dump(data, open(out, "w"), indent=1)
+    print(json.dumps(data, indent=1))
+
+
+if __name__ == "__main__":
+    main()
