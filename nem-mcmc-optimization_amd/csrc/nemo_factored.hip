@@ -423,11 +423,15 @@ hipError_t launch_fact_resident_t(Ctx& c, int batch, double* d_cs, double* d_cel
 
 __global__ void finalize_factored_kernel(int batch, int n, const double* __restrict__ partial,
                                          double* __restrict__ ll) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per evaluation: strided lane sums, then a fixed xor tree --
+  // bitwise reproducible, and ~n/64 dependent adds instead of n
+  const int b = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
   if (b >= batch) return;
   double s = 0.0;
-  for (int t = 0; t < n; ++t) s += partial[(size_t)b * n + t];
-  ll[b] = s;
+  for (int t = lane; t < n; t += kWave) s += partial[(size_t)b * n + t];
+  s = fwave_sum(s);
+  if (lane == 0) ll[b] = s;
 }
 
 template <int NR>
@@ -504,7 +508,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // per-evaluation partials: one per 16-effect tile (resident) or per wave
   // slot of the 128-effect blocks (chunked); summed in a fixed order
   const int np = resident ? (c.E + 15) / 16 : factored_partials(c);
-  finalize_factored_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, np, c.d_fpartial, d_ll);
+  finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
   return hipGetLastError();
 }
 

@@ -228,11 +228,15 @@ __global__ __launch_bounds__(kScoreWaves * kWave) void score_kernel(
 // ll[b] = sum over tiles (fixed order: bitwise reproducible)
 __global__ void finalize_kernel(int batch, int ntiles, const double* __restrict__ partial,
                                 double* __restrict__ ll) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // one wave per evaluation: strided lane sums then a fixed xor tree
+  // (bitwise reproducible)
+  const int b = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
   if (b >= batch) return;
   double s = 0.0;
-  for (int t = 0; t < ntiles; ++t) s += partial[(size_t)b * ntiles + t];
-  ll[b] = s;
+  for (int t = lane; t < ntiles; t += kWave) s += partial[(size_t)b * ntiles + t];
+  s = wave_sum(s);
+  if (lane == 0) ll[b] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -546,7 +550,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
     hipEventRecord(e1, st);
     c.launches++;
   }
-  finalize_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, nt, c.d_partial, d_ll);
+  finalize_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, nt, c.d_partial, d_ll);
   return hipGetLastError();
 }
 
@@ -611,7 +615,7 @@ hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStr
     hipEventRecord(e1, st);
     c.launches++;
   }
-  finalize_kernel<<<(batch + 63) / 64, 64, 0, st>>>(batch, c.ntiles(), c.d_partial, d_ll);
+  finalize_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, c.ntiles(), c.d_partial, d_ll);
   return hipGetLastError();
 }
 
