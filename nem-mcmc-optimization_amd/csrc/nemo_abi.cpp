@@ -245,12 +245,18 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
     elo[j] = exp(lo);
     ehi[j] = exp(hi);
   }
+  // the factored kernels' exp takes finite arguments: U must be finite too
+  for (size_t k = 0; k < (S + 1) * E && fact; ++k)
+    if (!isfinite(U[k]) || fabs(U[k]) > 1e9) fact = false;
   c.factored = fact;
   c.fspad = nemo::factored_spad(c.S);
   c.nwords = nwords;
   if (c.d_U64) hipFree(c.d_U64);
   c.d_U64 = nullptr;
-  HIPCHK(hipMalloc((void**)&c.d_U64, (S + 1) * E * 8));
+  // + one zeroed 16-effect tile: the pipelined factored kernel reads whole
+  // tiles unclamped (lanes past E are masked out of every result)
+  HIPCHK(hipMalloc((void**)&c.d_U64, ((S + 1) * E + 16) * 8));
+  HIPCHK(hipMemset(c.d_U64, 0, ((S + 1) * E + 16) * 8));
   HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
   if (fact) {
     if (c.d_D1w) hipFree(c.d_D1w);
@@ -528,8 +534,9 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.xcd_remap = value ? 1 : 0;
     return NEMO_OK;
   }
-  if (strcmp(name, "fact_resident") == 0) {
-    ctx->c.fact_resident = value < 0 ? 0 : value;  // 0 off; 1, 2, 4: min waves/SIMD
+  if (strcmp(name, "fact_kernel") == 0) {
+    if (value < 0 || value > 3) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in {0,1,2,3}", value);
+    ctx->c.fact_kernel = value;
     return NEMO_OK;
   }
   if (strcmp(name, "score_path") == 0) {
@@ -548,7 +555,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   if (strcmp(name, "xcd_remap") == 0) *value = c.xcd_remap;
   else if (strcmp(name, "score_path") == 0) *value = c.score_path;
   else if (strcmp(name, "factored") == 0) *value = c.factored ? 1 : 0;
-  else if (strcmp(name, "fact_resident") == 0) *value = c.fact_resident;
+  else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;
 }

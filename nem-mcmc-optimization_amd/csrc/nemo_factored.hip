@@ -26,6 +26,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 namespace nemo {
 
 namespace {
@@ -57,6 +59,35 @@ __device__ __forceinline__ double exp_tab(double x, const double* __restrict__ t
   p = fma(r, p, 1.0);
   return ldexp(p * tab[k & 63], k >> 6);
 }
+
+// exp(x) for finite x in [-1e12, ~0]: the same table and polynomial, with
+// the round-to-nearest of x*64/ln2 taken from the low word of
+// fma(x, 64/ln2, 1.5*2^52) -- no clamp, rint or cvt (3 VALU fewer).
+__device__ __forceinline__ double exp_fast(double x, const double* __restrict__ tab) {
+  constexpr double kInvLn2x64 = 92.332482616893656768;
+  constexpr double kLn2d64Hi = 1.0830424696223417e-02;
+  constexpr double kLn2d64Lo = 2.5728046223276690e-14;
+  constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+  const double t = fma(x, kInvLn2x64, kMagic);
+  const double kf = t - kMagic;
+  const int k = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
+  double r = fma(-kf, kLn2d64Hi, x);
+  r = fma(-kf, kLn2d64Lo, r);
+  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = fma(r, p, 1.0 / 6.0);
+  p = fma(r, p, 0.5);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+  return ldexp(p * tab[k & 63], k >> 6);
+}
+
+// value of the G column on padding rows (q >= S): cells of padding rows are
+// U[S][e] + kPadG, whose exp underflows to exactly 0 next to any real row
+constexpr double kPadG = -1.0e6;
+
+// tiles per wave of the pipelined kernel: fixed, so the tile -> wave ->
+// partial assignment (hence every bit of ll) does not depend on the batch
+constexpr int kPipeTilesPerWave = 8;
 
 __device__ __forceinline__ int fxcd_work_index(int L, int N, int remap) {
   if (!remap) return L;
@@ -110,10 +141,16 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
         d = hi - lo;
         glo = lo;
       }
-      if (p < SPAD) drow[p] = d;
+      if (p < SPAD && p != (q | 15)) drow[p] = d;
       gsum += fwave_sum(glo);
     }
-    if (lane == 0) G[(size_t)b * SPAD + q] = gsum;
+    if (lane == 0) {
+      G[(size_t)b * SPAD + q] = gsum;
+      // column 16r+15 of row block r is never a parent of rows 16r..16r+15:
+      // it carries G (the score kernels multiply it by 1), and a finite
+      // "no row" value on padding rows
+      drow[q | 15] = q < S ? gsum : kPadG;
+    }
   }
 }
 
@@ -124,7 +161,7 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
 template <int NR, int WAVES>
 __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
     int S, int E, int ntiles, int cap, const double* __restrict__ Dp,
-    const double* __restrict__ G, const int32_t* __restrict__ permo,
+    const int32_t* __restrict__ permo,
     const uint64_t* __restrict__ D1w, int nwords, const double* __restrict__ U,
     double* __restrict__ partial, double* __restrict__ cs_out, double* __restrict__ cells,
     double* __restrict__ ow, int remap) {
@@ -137,8 +174,7 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* A = lds;                                       // [SPAD][LDA]
   uint64_t* words = (uint64_t*)(A + SPAD * LDA);         // [SPAD][WPR]
-  double* Gs = (double*)(words + SPAD * WPR);            // [SPAD]
-  double* etab = Gs + SPAD;                              // [64] 2^(j/64)
+  double* etab = (double*)(words + SPAD * WPR);          // [64] 2^(j/64)
   int* perm_s = (int*)(etab + 64);                       // [SPAD]
 
   const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
@@ -156,12 +192,12 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
   const int word0 = e_blk >> 6;
   const int shift = (e_w0 >> 6) - word0;  // which of the block's words this wave reads
   const int bitpos = (e_w0 & 63) + col;
+  const uint32_t diag = lane >= 48 ? 1u : 0u;
 
   if (tid < 64) etab[tid] = exp2((double)tid * (1.0 / 64.0));
   for (int k = tid; k < SPAD; k += blockDim.x) {
     const int node = permo[(size_t)b * SPAD + k];
     perm_s[k] = node;
-    Gs[k] = G[(size_t)b * SPAD + k];
     for (int u = 0; u < WPR; ++u) {
       const int wi = word0 + u;
       words[k * WPR + u] = (node < S && wi < nwords) ? D1w[(size_t)node * nwords + wi] : 0ull;
@@ -187,23 +223,26 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
     }
     __syncthreads();
     // B fragments of this chunk: lane holds D1[parent at 4s + lane/16][its effect]
-    double bf[NS];
+    uint32_t bits[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int p = c0 + 4 * s + (lane >> 4);
       const uint64_t wd = words[p * WPR + shift];
-      bf[s] = (double)((wd >> bitpos) & 1ull);
+      bits[s] = (uint32_t)((wd >> bitpos) & 1ull);
     }
     // lower-triangular k-loop, fully static: row block r (positions
-    // 16r..16r+15) has parents only at positions <= 16r+14.  k-steps outer,
-    // row blocks inner, so consecutive MFMAs use independent accumulators.
+    // 16r..16r+15) has parents only at positions <= 16r+14, and column
+    // 16r+15 holds G (B = 1 there: lanes 48..63 of the diagonal k-step).
+    // k-steps outer, row blocks inner: consecutive MFMAs use independent
+    // accumulators.
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        if (c0 + 4 * s <= 16 * r + 14) {
+        if (c0 + 4 * s <= 16 * r + 12) {
+          const uint32_t bv = (c0 + 4 * s == 16 * r + 12) ? (bits[s] | diag) : bits[s];
           const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
-          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[s], acc[r], 0, 0, 0);
+          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)bv, acc[r], 0, 0, 0);
         }
       }
     }
@@ -219,7 +258,7 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
     for (int g = 0; g < 4; ++g) {
       const int q = 16 * r + (lane >> 4) + 4 * g;
       double v = -INFINITY;
-      if (q < S) v = U[(size_t)perm_s[q] * E + ec] + Gs[q] + acc[r][g];
+      if (q < S) v = U[(size_t)perm_s[q] * E + ec] + acc[r][g];
       cell[r][g] = v;
       m = v > m ? v : m;
     }
@@ -263,164 +302,6 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// resident variant (S <= 64): a block stages its evaluation's Delta, G, pi
-// and the D1 bits of its column range ONCE, then every wave walks its share
-// of 16-effect tiles with no further barrier.  Per tile the epilogue's U rows
-// are requested before the MFMA phase, so their latency hides under it.
-// grid = batch * split (split column ranges per evaluation), block = WAVES.
-// ---------------------------------------------------------------------------
-template <int NR, int WAVES, int MINW>
-__global__ __launch_bounds__(WAVES * kWave, MINW) void score_factored_resident_kernel(
-    int S, int E, int ntiles, int split, const double* __restrict__ Dp,
-    const double* __restrict__ G, const int32_t* __restrict__ permo,
-    const uint64_t* __restrict__ D1w, int nwords, const double* __restrict__ U,
-    double* __restrict__ partial, double* __restrict__ cs_out, double* __restrict__ cells,
-    double* __restrict__ ow, int remap) {
-  constexpr int SPAD = NR * 16;
-  constexpr int LDA = SPAD + 1;
-  constexpr int NS = SPAD / 4;
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tiles_per = (ntiles + split - 1) / split;     // 16-effect tiles per block
-  const int wpb = (tiles_per * 16 + 63) / 64 + 1;         // D1 words per row in the range
-  double* A = lds;                                        // [SPAD][LDA]
-  double* Gs = A + SPAD * LDA;                            // [SPAD]
-  double* etab = Gs + SPAD;                               // [64]
-  uint64_t* words = (uint64_t*)(etab + 64);               // [SPAD][wpb]
-  int* perm_s = (int*)(words + SPAD * wpb);               // [SPAD]
-
-  const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
-  const int b = work / split;
-  const int part_id = work - b * split;
-  const int t_begin = part_id * tiles_per;
-  const int t_end = min(ntiles, t_begin + tiles_per);
-  const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const int word0 = (t_begin * 16) >> 6;
-
-  if (tid < 64) etab[tid] = exp2((double)tid * (1.0 / 64.0));
-  for (int k = tid; k < SPAD; k += blockDim.x) {
-    const int node = permo[(size_t)b * SPAD + k];
-    perm_s[k] = node;
-    Gs[k] = G[(size_t)b * SPAD + k];
-    for (int u = 0; u < wpb; ++u) {
-      const int wi = word0 + u;
-      words[k * wpb + u] = (node < S && wi < nwords) ? D1w[(size_t)node * nwords + wi] : 0ull;
-    }
-  }
-  const double* Db = Dp + (size_t)b * SPAD * SPAD;
-  for (int k = tid; k < SPAD * SPAD; k += blockDim.x) {
-    const int row = k / SPAD, kk = k - row * SPAD;
-    if (kk <= (row | 15)) A[row * LDA + kk] = Db[k];
-  }
-  __syncthreads();
-
-  const int col = lane & 15;
-  for (int t = t_begin + w; t < t_end; t += WAVES) {
-    const int e_w0 = t * 16;
-    const int e = e_w0 + col;
-    const bool valid = e < E;
-    const int ec = valid ? e : E - 1;
-    // epilogue operands first: their latency hides under the MFMAs
-    double u[NR][4];
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int q = 16 * r + (lane >> 4) + 4 * g;
-        u[r][g] = (q < S) ? U[(size_t)perm_s[q] * E + ec] : 0.0;
-      }
-    const double unull = U[(size_t)S * E + ec];
-    const int widx = (e_w0 >> 6) - word0;
-    const int bitpos = (e_w0 & 63) + col;
-    f64x4 acc[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = f64x4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int p = 4 * s + (lane >> 4);
-      const double bf = (double)((words[p * wpb + widx] >> bitpos) & 1ull);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (4 * s <= 16 * r + 14) {
-          const double a = A[(16 * r + (lane & 15)) * LDA + 4 * s + (lane >> 4)];
-          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf, acc[r], 0, 0, 0);
-        }
-      }
-    }
-    double m = unull;
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int q = 16 * r + (lane >> 4) + 4 * g;
-        const double v = (q < S) ? u[r][g] + Gs[q] + acc[r][g] : -INFINITY;
-        u[r][g] = v;  // now the cell
-        m = v > m ? v : m;
-      }
-    m = fmax(m, __shfl_xor(m, 16, kWave));
-    m = fmax(m, __shfl_xor(m, 32, kWave));
-    double l = 0.0;
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) l += exp_tab(u[r][g] - m, etab);
-    l += __shfl_xor(l, 16, kWave);
-    l += __shfl_xor(l, 32, kWave);
-    l += exp_tab(unull - m, etab);
-    const double cs = m + log(l);
-    if (valid && lane < 16 && cs_out) cs_out[(size_t)b * E + e] = cs;
-    double part = (valid && lane < 16) ? cs : 0.0;
-    part = fwave_sum(part);
-    if (lane == 0) partial[(size_t)b * ntiles + t] = part;
-    if ((cells || ow) && valid) {
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int q = 16 * r + (lane >> 4) + 4 * g;
-          if (q < S) {
-            const size_t k = ((size_t)b * (S + 1) + perm_s[q]) * E + e;
-            if (cells) cells[k] = u[r][g];
-            if (ow) ow[k] = exp_tab(u[r][g] - cs, etab);
-          }
-        }
-      if (lane < 16) {
-        const size_t k = ((size_t)b * (S + 1) + S) * E + e;
-        if (cells) cells[k] = unull;
-        if (ow) ow[k] = exp_tab(unull - cs, etab);
-      }
-    }
-  }
-}
-
-template <int NR>
-hipError_t launch_fact_resident_t(Ctx& c, int batch, double* d_cs, double* d_cells, double* d_ow,
-                                  hipStream_t st) {
-  constexpr int WAVES = kFactWaves;
-  constexpr int SPAD = NR * 16;
-  const int ntiles = (c.E + 15) / 16;
-  // enough blocks to cover the CUs twice, each owning whole waves of tiles
-  int split = (2 * 256 + batch - 1) / batch;
-  const int max_split = (ntiles + WAVES - 1) / WAVES;
-  split = split < 1 ? 1 : (split > max_split ? max_split : split);
-  const int tiles_per = (ntiles + split - 1) / split;
-  const int wpb = (tiles_per * 16 + 63) / 64 + 1;
-  const size_t lds = (size_t)SPAD * (SPAD + 1) * 8 + SPAD * 8 + 64 * 8 + (size_t)SPAD * wpb * 8 +
-                     SPAD * 4;
-#define NEMO_FR(MINW)                                                                         \
-  score_factored_resident_kernel<NR, WAVES, MINW><<<dim3(batch * split), WAVES * kWave, lds, st>>>( \
-      c.S, c.E, ntiles, split, c.d_fDp, c.d_fG, c.d_fperm, c.d_D1w, c.nwords,                 \
-      (const double*)c.d_U64, c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap)
-  // option fact_resident = minimum waves per SIMD the register budget targets
-  if (c.fact_resident >= 4) NEMO_FR(4);
-  else if (c.fact_resident >= 2) NEMO_FR(2);
-  else NEMO_FR(1);
-#undef NEMO_FR
-  return hipGetLastError();
-}
-
 __global__ void finalize_factored_kernel(int batch, int n, const double* __restrict__ partial,
                                          double* __restrict__ ll) {
   // one wave per evaluation: strided lane sums, then a fixed xor tree --
@@ -434,23 +315,224 @@ __global__ void finalize_factored_kernel(int batch, int n, const double* __restr
   if (lane == 0) ll[b] = s;
 }
 
+// ---------------------------------------------------------------------------
+// pipelined kernel (SPAD <= 64, the C1-C3 shapes): a block owns one
+// evaluation x a contiguous range of 16-effect tiles and stages that
+// evaluation's Delta (+ G column) and the D1 words of its range ONCE; each
+// wave then walks its tiles (t_begin + w, + WAVES, ...) with no further
+// barrier, software-pipelined two deep:
+//     MFMA chain of tile i  ||  exp / log-sum-exp epilogue of tile i-1
+//     (+ the U loads of tile i+1 in flight)
+// The MFMA accumulators start at U[perm[q]][e] (the C operand), and the G
+// column rides in the diagonal k-step, so a cell leaves the MFMA complete.
+// Per tile the epilogue keeps sum(m) and prod(l) per column (l in [1, S+1],
+// the product as mantissa x 2^exp), so the log of the log-sum-exp runs once
+// per wave, not per tile.  ll only: calls that want cs / cells / order
+// weights take the chunked kernel.
+// ---------------------------------------------------------------------------
+template <int NR, int WAVES>
+__global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
+    int S, int E, int ntiles, int split, const double* __restrict__ Dp,
+    const int32_t* __restrict__ permo, const uint64_t* __restrict__ D1w, int nwords,
+    const double* __restrict__ U, double* __restrict__ partial, int remap) {
+  // block = (evaluation b, tile range [t_begin, t_begin + WAVES * 8))
+  constexpr int SPAD = NR * 16;
+  constexpr int LDA = SPAD + 1;  // odd row stride: conflict-free A fragments
+  constexpr int NS = SPAD / 4;
+  constexpr int NMFMA = NR * (NR + 1) * 2;       // MFMAs per tile (triangle)
+  constexpr int VPM = 8;                         // VALU slots per MFMA
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* A = lds;                               // [SPAD][LDA]
+  double* etab = A + SPAD * LDA;                 // [64] 2^(j/64)
+  uint64_t* words = (uint64_t*)(etab + 64);      // [nwb][SPAD] D1 words, word-major
+
+  const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / split;
+  const int part = work - b * split;
+  const int tpb = kPipeTilesPerWave * WAVES;
+  const int t_begin = part * tpb;
+  const int t_end = min(ntiles, t_begin + tpb);
+  const int w_lo = (t_begin * 16) >> 6;
+  const int nwb = t_end > t_begin ? (((t_end * 16 - 1) >> 6) - w_lo + 1) : 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int col = lane & 15, rg = lane >> 4;
+
+  const int32_t* pm = permo + (size_t)b * SPAD;
+  if (tid < 64) etab[tid] = exp2((double)tid * (1.0 / 64.0));
+  for (int k = tid; k < SPAD * nwb; k += blockDim.x) {
+    const int u = k / SPAD, p = k - u * SPAD;
+    const int node = pm[p];
+    const int wi = w_lo + u;
+    words[k] = (node < S && wi < nwords) ? D1w[(size_t)node * nwords + wi] : 0ull;
+  }
+  const double* Db = Dp + (size_t)b * SPAD * SPAD;
+  for (int k = tid; k < SPAD * SPAD; k += blockDim.x) {
+    const int row = k / SPAD, kk = k - row * SPAD;
+    if (kk <= (row | 15)) A[row * LDA + kk] = Db[k];
+  }
+  // byte offsets of this lane's 16 cells in U: row perm[q] (S = the
+  // "attached to nothing" row for padding), column = its effect in the tile
+  uint32_t uoff[NR][4];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      uoff[r][g] = ((uint32_t)pm[16 * r + rg + 4 * g] * (uint32_t)E + col) * 8u;
+  const uint32_t unoff = ((uint32_t)S * E + col) * 8u;
+  __syncthreads();
+
+  const int ntw = split * WAVES;
+  double* part_out = partial + (size_t)b * ntw + part * WAVES + w;
+  int t = t_begin + w;
+  if (t >= t_end) {
+    if (lane == 0) *part_out = 0.0;
+    return;
+  }
+
+  const uint32_t diag = lane >= 48 ? 1u : 0u;
+  const int arow = col * LDA + rg;
+  const uint32_t* w32 = (const uint32_t*)words;
+  const char* Ub = (const char*)U;
+
+  auto load_u = [&](int tt, double (&u)[NR][4], double& un) {
+    const char* base = Ub + (size_t)tt * 128;  // 16 effects x 8 B (uniform)
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) u[r][g] = *(const double*)(base + uoff[r][g]);
+    un = *(const double*)(base + unoff);
+  };
+  auto mfma_tile = [&](int tt, const double (&u)[NR][4], f64x4 (&acc)[NR]) {
+    const int uidx = ((tt * 16) >> 6) - w_lo;
+    const int half = (tt >> 1) & 1;
+    const uint32_t bit = ((tt & 1) << 4) + col;
+    const uint32_t* wp = w32 + ((size_t)uidx * SPAD + rg) * 2 + half;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = f64x4{u[r][0], u[r][1], u[r][2], u[r][3]};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint32_t bv = __builtin_amdgcn_ubfe(wp[8 * s], bit, 1);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        if (4 * s <= 16 * r + 12) {
+          const uint32_t bb = (4 * s == 16 * r + 12) ? (bv | diag) : bv;
+          const double a = A[arow + 16 * r * LDA + 4 * s];
+          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)bb, acc[r], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  double msum = 0.0, lprod = 1.0;
+  int lexp = 0;
+  auto epilogue = [&](int tt, const f64x4 (&acc)[NR], double unull) {
+    const int e = tt * 16 + col;
+    const bool valid = e < E;
+    double m = unull;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) m = fmax(m, acc[r][g]);
+    m = fmax(m, __shfl_xor(m, 16, kWave));
+    m = fmax(m, __shfl_xor(m, 32, kWave));
+    double l = 0.0;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) l += exp_fast(acc[r][g] - m, etab);
+    l += __shfl_xor(l, 16, kWave);
+    l += __shfl_xor(l, 32, kWave);
+    l += exp_fast(unull - m, etab);
+    {
+      // prod(l) kept as mantissa * 2^lexp: branch-free, no overflow
+      msum += valid ? m : 0.0;
+      lprod *= valid ? l : 1.0;
+      const int ex = __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      lexp += ex;
+    }
+    {
+      // interleave this epilogue's VALU with the next tile's MFMA chain
+#pragma unroll
+      for (int i = 0; i < NMFMA; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);  // VALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+    }
+  };
+
+  // two-deep software pipeline, unrolled twice so the accumulators swap roles
+  // without register copies
+  double uc[NR][4], unc;
+  f64x4 accA[NR], accB[NR];
+  double nulA, nulB;
+  load_u(t, uc, unc);
+  mfma_tile(t, uc, accA);
+  nulA = unc;
+  int tp = t;
+  t += WAVES;
+  if (t < t_end) load_u(t, uc, unc);
+  bool a_pending = true;
+  while (t < t_end) {
+    mfma_tile(t, uc, accB);
+    nulB = unc;
+    load_u(min(t + WAVES, t_end - 1), uc, unc);  // clamped: no branch in the block
+    epilogue(tp, accA, nulA);
+    tp = t;
+    t += WAVES;
+    if (t >= t_end) {
+      a_pending = false;
+      break;
+    }
+    mfma_tile(t, uc, accA);
+    nulA = unc;
+    load_u(min(t + WAVES, t_end - 1), uc, unc);
+    epilogue(tp, accB, nulB);
+    tp = t;
+    t += WAVES;
+  }
+  if (a_pending) epilogue(tp, accA, nulA);
+  else epilogue(tp, accB, nulB);
+
+  double v = msum + (log(lprod) + (double)lexp * 0.69314718055994530942);
+  v = lane < 16 ? v : 0.0;
+  v = fwave_sum(v);
+  if (lane == 0) *part_out = v;
+}
+
 template <int NR>
-hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_ll, double* d_cs, double* d_cells,
-                         double* d_ow, hipStream_t st) {
+hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_cs, double* d_cells,
+                         double* d_ow, hipStream_t st, int* nparts) {
   constexpr int WAVES = kFactWaves;
   constexpr int SPAD = NR * 16;
   constexpr int KC = SPAD < 64 ? SPAD : 64;
   constexpr int COLS = WAVES * 16;
   constexpr int WPR = (COLS + 63) / 64 + 1;
   const int nt = (c.E + COLS - 1) / COLS;
-  const size_t lds = (size_t)SPAD * (KC + 1) * 8 + (size_t)SPAD * WPR * 8 + SPAD * 8 + 64 * 8 +
-                     SPAD * 4;
+  const size_t lds = (size_t)SPAD * (KC + 1) * 8 + (size_t)SPAD * WPR * 8 + 64 * 8 + SPAD * 4;
   score_factored_kernel<NR, WAVES><<<dim3(nt * batch), WAVES * kWave, lds, st>>>(
-      c.S, c.E, nt, cap, c.d_fDp, c.d_fG, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
+      c.S, c.E, nt, cap, c.d_fDp, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
       c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
-  return hipSuccess;
+  *nparts = nt * WAVES;
+  return hipGetLastError();
+}
+
+template <int NR, int WAVES>
+hipError_t launch_pipe_t(Ctx& c, int batch, hipStream_t st, int* nparts) {
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  const int tpb = kPipeTilesPerWave * WAVES;
+  const int split = (ntiles + tpb - 1) / tpb;
+  const int nwb_max = (tpb * 16 + 63) / 64 + 1;
+  const size_t lds = (size_t)SPAD * (SPAD + 1) * 8 + 64 * 8 + (size_t)nwb_max * SPAD * 8;
+  score_factored_pipe_kernel<NR, WAVES><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+      c.S, c.E, ntiles, split, c.d_fDp, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
+      c.d_fpartial, c.xcd_remap);
+  *nparts = split * WAVES;
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -464,8 +546,13 @@ int factored_spad(int S) {
 }
 
 int factored_partials(const Ctx& c) {
+  // chunked: one per wave slot of the 128-effect blocks; pipelined: one per
+  // wave of ceil(tiles / (8 * waves)) blocks, waves in {4, 8}
   const int cols = kFactWaves * 16;
-  return ((c.E + cols - 1) / cols) * kFactWaves;
+  const int nt = (c.E + 15) / 16;
+  int n = ((c.E + cols - 1) / cols) * kFactWaves;
+  for (int wv : {4, 8}) n = std::max(n, ((nt + kPipeTilesPerWave * wv - 1) / (kPipeTilesPerWave * wv)) * wv);
+  return n;
 }
 
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
@@ -482,21 +569,32 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     e1 = c.ev_pool[c.ev_used++];
     hipEventRecord(e0, st);
   }
-  const bool resident = c.fact_resident && spad <= 64;
-  if (resident) {
+  // option fact_kernel: 0 auto (pipelined for ll-only calls with S <= 64),
+  // 1 chunked, 2 pipelined with 4 waves per block, 3 pipelined with 8
+  const int fk = c.fact_kernel;
+  const bool pipe = spad <= 64 && fk != 1 && !d_cs && !d_cells && !d_ow;
+  int np = 0;
+  if (pipe) {
+    const bool w8 = fk == 3;
     switch (spad / 16) {
-      case 1: err = launch_fact_resident_t<1>(c, batch, d_cs, d_cells, d_ow, st); break;
-      case 2: err = launch_fact_resident_t<2>(c, batch, d_cs, d_cells, d_ow, st); break;
-      case 4: err = launch_fact_resident_t<4>(c, batch, d_cs, d_cells, d_ow, st); break;
+#define NEMO_PIPE(NRV)                                                               \
+  case NRV:                                                                          \
+    err = w8 ? launch_pipe_t<NRV, 8>(c, batch, st, &np)                              \
+             : launch_pipe_t<NRV, 4>(c, batch, st, &np);                             \
+    break;
+      NEMO_PIPE(1)
+      NEMO_PIPE(2)
+      NEMO_PIPE(4)
+#undef NEMO_PIPE
       default: return hipErrorInvalidValue;
     }
   } else {
     switch (spad / 16) {
-      case 1: err = launch_fact_t<1>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-      case 2: err = launch_fact_t<2>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-      case 4: err = launch_fact_t<4>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-      case 8: err = launch_fact_t<8>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
-      case 16: err = launch_fact_t<16>(c, batch, cap, d_ll, d_cs, d_cells, d_ow, st); break;
+      case 1: err = launch_fact_t<1>(c, batch, cap, d_cs, d_cells, d_ow, st, &np); break;
+      case 2: err = launch_fact_t<2>(c, batch, cap, d_cs, d_cells, d_ow, st, &np); break;
+      case 4: err = launch_fact_t<4>(c, batch, cap, d_cs, d_cells, d_ow, st, &np); break;
+      case 8: err = launch_fact_t<8>(c, batch, cap, d_cs, d_cells, d_ow, st, &np); break;
+      case 16: err = launch_fact_t<16>(c, batch, cap, d_cs, d_cells, d_ow, st, &np); break;
       default: return hipErrorInvalidValue;
     }
   }
@@ -505,9 +603,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     (void)hipEventRecord(e1, st);
     c.launches++;
   }
-  // per-evaluation partials: one per 16-effect tile (resident) or per wave
-  // slot of the 128-effect blocks (chunked); summed in a fixed order
-  const int np = resident ? (c.E + 15) / 16 : factored_partials(c);
+  // per-evaluation partials, summed in a fixed order
   finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
   return hipGetLastError();
 }

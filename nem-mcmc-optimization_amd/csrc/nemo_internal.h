@@ -52,7 +52,7 @@ struct Ctx {
   // factored (MFMA) path: available when every off-diagonal table row is
   // shared by all children and two-valued (all tables nem.py builds)
   int score_path = 0;              // option "score_path": 0 auto, 1 stream, 2 factored
-  int fact_resident = 0;           // option "fact_resident": S <= 64 resident-Delta kernel
+  int fact_kernel = 0;             // option "fact_kernel": 0 auto, 1 chunked, 2/3 pipelined (4/8 waves)
   bool factored = false;
   int fspad = 0;                   // S rounded up to the MFMA row-block size
   int nwords = 0;                  // 64-bit words per D1 row

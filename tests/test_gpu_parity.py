@@ -58,9 +58,12 @@ def test_score_net2_golden(net2_engine):
     for c in range(len(pos)):
         cell = no.cell_ratios(t["U"], t["T"], no.parents_of(z["perm"][c]), w01[c])
         assert np.max(np.abs(out["cells"][c] - cell)) <= 1e-11
-    # single-eval calls give the same bits as the batch
+    # ll-only calls (the pipelined kernel) agree with the full-output kernel,
+    # and single-eval calls give the same bits as the batch
+    ll = eng.score(pos, w01)
+    assert np.max(np.abs(ll - out["ll"])) <= 1e-9
     for c in (0, 5):
-        assert eng.score(pos[c:c + 1], w01[c:c + 1])[0] == out["ll"][c]
+        assert eng.score(pos[c:c + 1], w01[c:c + 1])[0] == ll[c]
 
 
 @pytest.mark.parametrize("name,s,e", [("C2", 16, 500), ("C3", 64, 2000)])
@@ -308,3 +311,40 @@ def test_factored_detection_rejects_generic_tables():
     w01 = rng.random((s, s))
     ll = eng.score(_pos(perm)[None], w01[None])[0]
     assert abs(ll - no.order_score(u, t, perm, w01)) <= 1e-9
+
+
+@pytest.mark.parametrize("s,e", [(2, 1), (11, 184), (16, 500), (33, 17), (40, 333), (64, 2000)])
+def test_factored_kernel_variants_agree(s, e):
+    """Chunked (fact_kernel=1) and pipelined (2: 4 waves, 3: 8 waves) factored
+    kernels against the streaming kernel and the oracle: padding rows
+    (S % 16 != 0), ragged last tile (E % 16 != 0), tiny E; the pipelined
+    kernel's bits do not depend on the batch size."""
+    m = generator.synthetic_nem(s, e, 3)
+    t = m.get_score_tensor()
+    eng = Engine(m.U, t)
+    assert eng.factored
+    rng = np.random.default_rng(s + e)
+    b = 37
+    perms = [rng.permutation(s) for _ in range(b)]
+    pos = np.array([_pos(p) for p in perms])
+    w01 = expit(rng.uniform(-4, 4, (b, s, s)))
+    eng.set_option("score_path", 1)
+    ref = eng.score(pos, w01)
+    eng.set_option("score_path", 2)
+    for fk in (1, 2, 3):
+        eng.set_option("fact_kernel", fk)
+        ll = eng.score(pos, w01)
+        assert np.max(np.abs(ll - ref)) <= 1e-9, fk
+        for c in (0, 11, 36):
+            assert eng.score(pos[c:c + 1], w01[c:c + 1])[0] == ll[c]
+    for c in (0, 1):
+        assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-9
+    # zero and one weights (G, Delta at their extremes)
+    for w in (0.0, 1.0):
+        wz = np.full((2, s, s), w)
+        eng.set_option("fact_kernel", 2)
+        a = eng.score(pos[:2], wz)
+        eng.set_option("score_path", 1)
+        assert np.max(np.abs(a - eng.score(pos[:2], wz))) <= 1e-9
+        eng.set_option("score_path", 2)
+    eng.close()

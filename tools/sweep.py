@@ -36,13 +36,13 @@ def main():
         S, E, seed, cap, dtype = generator.CONFIGS[cfg]
         m = generator.config_nem(cfg)
         eng = Engine.for_nem(m, dtype=dtype)
+        # (batch, group, xcd_remap, path): path 1 = stream, 2 + 10 * fact_kernel = factored
         variants = []
         for batch in (32, 128, 512):
-            for group in ((1, 4, 8) if cap == 0 else (1,)):
-                for remap in (0, 1):
-                    variants.append((batch, group, remap, 1))
-            for fr in (0, 1, 4):                # factored MFMA path, fact_resident
-                variants.append((batch, 1, 1, 2 + 10 * fr))
+            for group in ((1, 8) if cap == 0 else (1,)):
+                variants.append((batch, group, 1, 1))
+            for fk in (1, 2, 3):                # chunked, pipelined x4 waves, pipelined x8
+                variants.append((batch, 1, 1, 2 + 10 * fk))
         maxb = max(v[0] for v in variants)
         eng.reserve(maxb)
         rng = np.random.default_rng(5)
@@ -56,7 +56,7 @@ def main():
                 batch, group, remap, path = v
                 eng.set_option("xcd_remap", remap)
                 eng.set_option("score_path", path % 10)
-                eng.set_option("fact_resident", path // 10)
+                eng.set_option("fact_kernel", path // 10)
                 eng.score_dev(batch, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(), cap=cap, stream=st, group=group)
             torch.cuda.synchronize()
             for _ in range(args.rounds):
@@ -64,7 +64,7 @@ def main():
                     batch, group, remap, path = v
                     eng.set_option("xcd_remap", remap)
                     eng.set_option("score_path", path % 10)
-                    eng.set_option("fact_resident", path // 10)
+                    eng.set_option("fact_kernel", path // 10)
                     eng.timing(True)
                     for _ in range(args.steps):
                         eng.score_dev(batch, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(), cap=cap,
@@ -76,12 +76,12 @@ def main():
         for v, ts in times.items():
             batch, group, remap, path = v
             med = float(np.median(ts))
-            name = f"factored fr={path // 10}" if path % 10 == 2 else "stream"
+            name = f"factored fk={path // 10}" if path % 10 == 2 else "stream"
             results[f"{cfg} b={batch} g={group} remap={remap} path={name}"] = {
                 "median_ms": med, "min_ms": float(np.min(ts)),
                 "evals_per_s_kernel": batch / (med / 1e3)}
         eng.set_option("score_path", 0)
-        eng.set_option("fact_resident", 1)
+        eng.set_option("fact_kernel", 0)
         eng.set_option("xcd_remap", 1)
         # fused per-step scorer (eval #1 + local optima + eval #2)
         from nemo.nem_order_mcmc import SIG0, SIG1
