@@ -196,13 +196,19 @@ def main():
         if factored:
             fpe = algorithmic_flops_per_eval(S, E, cap)
             ach = B * fpe / (kern_ms / 1e3) / 1e12
+            i8 = S <= 64 and eng.get_option("fact_kernel") in (0, 4, 5, 6, 7)
+            kname = ("score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
+                     "fp64 cells + fused log-sum-exp)" if i8 else
+                     "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)")
             roof = {"bound": "mfma", "achieved": ach, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": ach / F64_MFMA_PEAK_TF,
-                    "traffic": load_traffic(f"{args.config}:factored:b{B}"),
-                    "kernel": "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)",
-                    "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
-                    "note": "FLOPs of the dense contraction Delta.D1 over the permissible pairs; "
-                            "the fused log-sum-exp epilogue (S+1)*E exps/eval is VALU work on top"}
+                    "traffic": load_traffic(f"{args.config}:{'i8' if i8 else 'factored'}:b{B}"),
+                    "kernel": kname, "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
+                    "note": "achieved = the algorithmic fp64 contraction Delta.D1 over the permissible "
+                            "pairs (2*P*E FLOP/eval) per kernel second, priced against the dense fp64 "
+                            "MFMA peak; the int8 kernel computes it exactly in 48-bit fixed point "
+                            "(DESIGN.md 3.1b) and is limited by the fp64 VALU of the fused "
+                            "log-sum-exp epilogue ((S+1)*E exps/eval)"}
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
             ach = B * bpe / (kern_ms / 1e3) / 1e9

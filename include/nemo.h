@@ -134,8 +134,10 @@ int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
  *                shared by all children and two-valued), else the streaming
  *                kernel; 1 = always stream; 2 = always factored
  *   "fact_kernel" 0 (default) auto: ll-only calls with S <= 64 take the
- *                pipelined factored kernel, the rest the chunked one;
- *                1 = chunked; 2 / 3 = pipelined with 4 / 8 waves per block
+ *                int8 fixed-point factored kernel, the rest the chunked fp64
+ *                one; 1 = chunked; 2 / 3 = fp64 pipelined with 4 / 8 waves
+ *                per block; 4 / 5 = int8 with 4 / 5 digit pairs; 6 = int8
+ *                with 8 waves per block; 7 = int8, A fragments in registers
  *   "factored"   (get only) 1 if the staged table is factorable */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);

@@ -127,7 +127,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
-                  c.d_fpartial};
+                  c.d_fpartial, c.d_B8, c.d_fD8};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -158,6 +158,7 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_fG, nb * sp));
     HIPCHK(dalloc(&c.d_fperm, nb * sp));
     HIPCHK(dalloc(&c.d_fpartial, nb * (size_t)nemo::factored_partials(c)));
+    if (sp <= 64) HIPCHK(dalloc(&c.d_fD8, nb * (size_t)(2 * nemo::kI8MaxPairs) * sp * 64));
     c.cap_batch = nb;
   }
   const int nc = std::max(max_chains, 1);
@@ -253,10 +254,12 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
   c.nwords = nwords;
   if (c.d_U64) hipFree(c.d_U64);
   c.d_U64 = nullptr;
-  // + one zeroed 16-effect tile: the pipelined factored kernel reads whole
-  // tiles unclamped (lanes past E are masked out of every result)
-  HIPCHK(hipMalloc((void**)&c.d_U64, ((S + 1) * E + 16) * 8));
-  HIPCHK(hipMemset(c.d_U64, 0, ((S + 1) * E + 16) * 8));
+  // rows up to the factored row padding (zero; the int8 kernel reads padding
+  // rows unclamped, their G hides them) + one zeroed 16-effect tile (the
+  // factored kernels read whole tiles; lanes past E are masked out)
+  const size_t urows = std::max(S + 1, (size_t)std::max(nemo::factored_spad(c.S), 0));
+  HIPCHK(hipMalloc((void**)&c.d_U64, (urows * E + 16) * 8));
+  HIPCHK(hipMemset(c.d_U64, 0, (urows * E + 16) * 8));
   HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
   if (fact) {
     if (c.d_D1w) hipFree(c.d_D1w);
@@ -268,6 +271,31 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
     HIPCHK(hipMemcpy(c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
+    // int8 variant (S <= 64): per-model fixed-point scale and the D1 bytes in
+    // v_mfma_i32_16x16x64_i8 B-fragment order: tile t, lane l (effect
+    // 16t + (l & 15), parents 16 (l >> 4) .. + 15), byte j = parent 16 (l >> 4) + j
+    if (c.d_B8) hipFree(c.d_B8);
+    c.d_B8 = nullptr;
+    if (S <= 64) {
+      double dmax = 0.0;
+      for (size_t j = 0; j < S; ++j) dmax = std::max(dmax, fabs(log(ehi[j]) - log(elo[j])));
+      int ex = 0;
+      if (dmax > 0.0) frexp(dmax * (1.0 + 1e-9), &ex);  // dmax * (1 + 1e-9) <= 2^ex
+      c.i8_cexp = dmax > 0.0 ? ex + 1 : 0;              // |Delta| <= 2^(c - 1)
+      const size_t nt = (E + 15) / 16;
+      std::vector<uint8_t> b8(nt * 64 * 16, 0);
+      for (size_t t = 0; t < nt; ++t)
+        for (int l = 0; l < 64; ++l) {
+          const size_t e = 16 * t + (l & 15);
+          if (e >= E) continue;
+          for (int jj = 0; jj < 16; ++jj) {
+            const size_t k = 16 * (l >> 4) + jj;
+            if (k < S) b8[(t * 64 + l) * 16 + jj] = (uint8_t)((d1[k * nwords + e / 64] >> (e % 64)) & 1ull);
+          }
+        }
+      HIPCHK(hipMalloc((void**)&c.d_B8, b8.size()));
+      HIPCHK(hipMemcpy(c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
+    }
   }
   // grow the factored scratch if a batch was reserved before staging
   if (c.cap_batch > 0) {
@@ -535,7 +563,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 3) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in {0,1,2,3}", value);
+    if (value < 0 || value > 7) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..7", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }

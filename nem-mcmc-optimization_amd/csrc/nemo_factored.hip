@@ -60,25 +60,33 @@ __device__ __forceinline__ double exp_tab(double x, const double* __restrict__ t
   return ldexp(p * tab[k & 63], k >> 6);
 }
 
-// exp(x) for finite x in [-1e12, ~0]: the same table and polynomial, with
-// the round-to-nearest of x*64/ln2 taken from the low word of
-// fma(x, 64/ln2, 1.5*2^52) -- no clamp, rint or cvt (3 VALU fewer).
-__device__ __forceinline__ double exp_fast(double x, const double* __restrict__ tab) {
-  constexpr double kInvLn2x64 = 92.332482616893656768;
-  constexpr double kLn2d64Hi = 1.0830424696223417e-02;
-  constexpr double kLn2d64Lo = 2.5728046223276690e-14;
-  constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
-  const double t = fma(x, kInvLn2x64, kMagic);
+// exp(x) for finite x in [-1e12, ~0] (the log-sum-exp terms): 256-entry
+// table of 2^(j/256) and a degree-4 polynomial on |r| <= ln2/512 (truncation
+// < 4e-17).  k = round(x * 256/ln2) comes from the low word of
+// fma(x, 256/ln2, 1.5*2^52) (no clamp, rint or cvt), and the reduction uses
+// one constant: its error, |x| * 1.6e-16 relative, is weighted by e^x in the
+// sum (< 1e-16 of it).  9 f64 VALU + 3 integer.
+__device__ __forceinline__ double exp_lse(double x, const double* __restrict__ tab) {
+  constexpr double kInvLn2x256 = 369.32993046757462707;  // 256 / ln 2
+  constexpr double kLn2d256 = 2.7076061740622862e-03;    // ln 2 / 256
+  constexpr double kMagic = 6755399441055744.0;          // 1.5 * 2^52
+  const double t = fma(x, kInvLn2x256, kMagic);
   const double kf = t - kMagic;
   const int k = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
-  double r = fma(-kf, kLn2d64Hi, x);
-  r = fma(-kf, kLn2d64Lo, r);
-  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  p = fma(r, p, 1.0 / 6.0);
+  const double r = fma(-kf, kLn2d256, x);
+  double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
   p = fma(r, p, 0.5);
   p = fma(r, p, 1.0);
   p = fma(r, p, 1.0);
-  return ldexp(p * tab[k & 63], k >> 6);
+  return ldexp(p * tab[k & 255], k >> 8);
+}
+
+// v_max_f64 without the sNaN canonicalisation hipcc wraps around fmax: the
+// operands here are MFMA results and loads of finite tables
+__device__ __forceinline__ double vmax(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 // value of the G column on padding rows (q >= S): cells of padding rows are
@@ -88,6 +96,9 @@ constexpr double kPadG = -1.0e6;
 // tiles per wave of the pipelined kernel: fixed, so the tile -> wave ->
 // partial assignment (hence every bit of ll) does not depend on the batch
 constexpr int kPipeTilesPerWave = 8;
+
+// fact_kernel = 0 (auto) resolves to this for ll-only calls with S <= 64
+constexpr int kAutoFactKernel = 4;
 
 __device__ __forceinline__ int fxcd_work_index(int L, int N, int remap) {
   if (!remap) return L;
@@ -320,9 +331,9 @@ __global__ void finalize_factored_kernel(int batch, int n, const double* __restr
 // evaluation x a contiguous range of 16-effect tiles and stages that
 // evaluation's Delta (+ G column) and the D1 words of its range ONCE; each
 // wave then walks its tiles (t_begin + w, + WAVES, ...) with no further
-// barrier, software-pipelined two deep:
-//     MFMA chain of tile i  ||  exp / log-sum-exp epilogue of tile i-1
-//     (+ the U loads of tile i+1 in flight)
+// barrier; the U rows of the next tile are prefetched.  (On gfx950 the f64
+// MFMA pipe and the VALU do not overlap -- tools/ubench/overlap.hip -- so
+// the cost is MFMA cycles + VALU cycles, and the epilogue is kept lean.)
 // The MFMA accumulators start at U[perm[q]][e] (the C operand), and the G
 // column rides in the diagonal k-step, so a cell leaves the MFMA complete.
 // Per tile the epilogue keeps sum(m) and prod(l) per column (l in [1, S+1],
@@ -337,14 +348,12 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
     const double* __restrict__ U, double* __restrict__ partial, int remap) {
   // block = (evaluation b, tile range [t_begin, t_begin + WAVES * 8))
   constexpr int SPAD = NR * 16;
-  constexpr int LDA = SPAD + 1;  // odd row stride: conflict-free A fragments
+  constexpr int LDA = SPAD + 2;  // == 2 mod 32: conflict-free b64 A fragments
   constexpr int NS = SPAD / 4;
-  constexpr int NMFMA = NR * (NR + 1) * 2;       // MFMAs per tile (triangle)
-  constexpr int VPM = 8;                         // VALU slots per MFMA
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* A = lds;                               // [SPAD][LDA]
-  double* etab = A + SPAD * LDA;                 // [64] 2^(j/64)
-  uint64_t* words = (uint64_t*)(etab + 64);      // [nwb][SPAD] D1 words, word-major
+  double* etab = lds;                            // [256] 2^(j/256)
+  double* A = etab + 256;                        // [SPAD][LDA]
+  uint64_t* words = (uint64_t*)(A + SPAD * LDA); // [nwb][SPAD] D1 words, word-major
 
   const int work = fxcd_work_index((int)blockIdx.x, (int)gridDim.x, remap);
   const int b = work / split;
@@ -360,7 +369,7 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
   const int col = lane & 15, rg = lane >> 4;
 
   const int32_t* pm = permo + (size_t)b * SPAD;
-  if (tid < 64) etab[tid] = exp2((double)tid * (1.0 / 64.0));
+  for (int k = tid; k < 256; k += blockDim.x) etab[k] = exp2((double)k * (1.0 / 256.0));
   for (int k = tid; k < SPAD * nwb; k += blockDim.x) {
     const int u = k / SPAD, p = k - u * SPAD;
     const int node = pm[p];
@@ -396,6 +405,7 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
   const uint32_t* w32 = (const uint32_t*)words;
   const char* Ub = (const char*)U;
 
+  // U rows of tile tt: the MFMA chain's C-init (prefetched one tile ahead)
   auto load_u = [&](int tt, double (&u)[NR][4], double& un) {
     const char* base = Ub + (size_t)tt * 128;  // 16 effects x 8 B (uniform)
 #pragma unroll
@@ -404,99 +414,60 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
       for (int g = 0; g < 4; ++g) u[r][g] = *(const double*)(base + uoff[r][g]);
     un = *(const double*)(base + unoff);
   };
-  auto mfma_tile = [&](int tt, const double (&u)[NR][4], f64x4 (&acc)[NR]) {
-    const int uidx = ((tt * 16) >> 6) - w_lo;
-    const int half = (tt >> 1) & 1;
-    const uint32_t bit = ((tt & 1) << 4) + col;
-    const uint32_t* wp = w32 + ((size_t)uidx * SPAD + rg) * 2 + half;
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] = f64x4{u[r][0], u[r][1], u[r][2], u[r][3]};
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t bv = __builtin_amdgcn_ubfe(wp[8 * s], bit, 1);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        if (4 * s <= 16 * r + 12) {
-          const uint32_t bb = (4 * s == 16 * r + 12) ? (bv | diag) : bv;
-          const double a = A[arow + 16 * r * LDA + 4 * s];
-          acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)bb, acc[r], 0, 0, 0);
-        }
-      }
-    }
-  };
 
   double msum = 0.0, lprod = 1.0;
   int lexp = 0;
-  auto epilogue = [&](int tt, const f64x4 (&acc)[NR], double unull) {
-    const int e = tt * 16 + col;
-    const bool valid = e < E;
+  double uc[NR][4], unc;
+  load_u(t, uc, unc);
+  for (; t < t_end; t += WAVES) {
+    // ---- cells of tile t: U + G + Delta . D1 on the MFMA (G rides in the
+    // diagonal k-step: column 16r+15 of row block r, B = 1 in lanes 48..63)
+    f64x4 acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = f64x4{uc[r][0], uc[r][1], uc[r][2], uc[r][3]};
+    const double unull = unc;
+    {
+      const int uidx = ((t * 16) >> 6) - w_lo;
+      const int half = (t >> 1) & 1;
+      const uint32_t bit = ((t & 1) << 4) + col;
+      const uint32_t* wp = w32 + ((size_t)uidx * SPAD + rg) * 2 + half;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t bv = __builtin_amdgcn_ubfe(wp[8 * s], bit, 1);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          if (4 * s <= 16 * r + 12) {
+            const uint32_t bb = (4 * s == 16 * r + 12) ? (bv | diag) : bv;
+            const double a = A[arow + 16 * r * LDA + 4 * s];
+            acc[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, (double)bb, acc[r], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (t + WAVES < t_end) load_u(t + WAVES, uc, unc);
+    // ---- column log-sum-exp (over the NR*16 rows and the null row)
+    const bool valid = t * 16 + col < E;
     double m = unull;
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) m = fmax(m, acc[r][g]);
-    m = fmax(m, __shfl_xor(m, 16, kWave));
-    m = fmax(m, __shfl_xor(m, 32, kWave));
+      for (int g = 0; g < 4; ++g) m = vmax(m, acc[r][g]);
+    m = vmax(m, __shfl_xor(m, 16, kWave));
+    m = vmax(m, __shfl_xor(m, 32, kWave));
     double l = 0.0;
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) l += exp_fast(acc[r][g] - m, etab);
+      for (int g = 0; g < 4; ++g) l += exp_lse(acc[r][g] - m, etab);
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
-    l += exp_fast(unull - m, etab);
-    {
-      // prod(l) kept as mantissa * 2^lexp: branch-free, no overflow
-      msum += valid ? m : 0.0;
-      lprod *= valid ? l : 1.0;
-      const int ex = __builtin_amdgcn_frexp_exp(lprod);
-      lprod = __builtin_amdgcn_frexp_mant(lprod);
-      lexp += ex;
-    }
-    {
-      // interleave this epilogue's VALU with the next tile's MFMA chain
-#pragma unroll
-      for (int i = 0; i < NMFMA; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);  // VALU
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-      }
-    }
-  };
-
-  // two-deep software pipeline, unrolled twice so the accumulators swap roles
-  // without register copies
-  double uc[NR][4], unc;
-  f64x4 accA[NR], accB[NR];
-  double nulA, nulB;
-  load_u(t, uc, unc);
-  mfma_tile(t, uc, accA);
-  nulA = unc;
-  int tp = t;
-  t += WAVES;
-  if (t < t_end) load_u(t, uc, unc);
-  bool a_pending = true;
-  while (t < t_end) {
-    mfma_tile(t, uc, accB);
-    nulB = unc;
-    load_u(min(t + WAVES, t_end - 1), uc, unc);  // clamped: no branch in the block
-    epilogue(tp, accA, nulA);
-    tp = t;
-    t += WAVES;
-    if (t >= t_end) {
-      a_pending = false;
-      break;
-    }
-    mfma_tile(t, uc, accA);
-    nulA = unc;
-    load_u(min(t + WAVES, t_end - 1), uc, unc);
-    epilogue(tp, accB, nulB);
-    tp = t;
-    t += WAVES;
+    l += exp_lse(unull - m, etab);
+    // prod(l) kept as mantissa * 2^lexp: branch-free, no overflow
+    msum += valid ? m : 0.0;
+    lprod *= valid ? l : 1.0;
+    lexp += __builtin_amdgcn_frexp_exp(lprod);
+    lprod = __builtin_amdgcn_frexp_mant(lprod);
   }
-  if (a_pending) epilogue(tp, accA, nulA);
-  else epilogue(tp, accB, nulB);
-
   double v = msum + (log(lprod) + (double)lexp * 0.69314718055994530942);
   v = lane < 16 ? v : 0.0;
   v = fwave_sum(v);
@@ -527,7 +498,7 @@ hipError_t launch_pipe_t(Ctx& c, int batch, hipStream_t st, int* nparts) {
   const int tpb = kPipeTilesPerWave * WAVES;
   const int split = (ntiles + tpb - 1) / tpb;
   const int nwb_max = (tpb * 16 + 63) / 64 + 1;
-  const size_t lds = (size_t)SPAD * (SPAD + 1) * 8 + 64 * 8 + (size_t)nwb_max * SPAD * 8;
+  const size_t lds = 256 * 8 + (size_t)SPAD * (SPAD + 2) * 8 + (size_t)nwb_max * SPAD * 8;
   score_factored_pipe_kernel<NR, WAVES><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, split, c.d_fDp, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
       c.d_fpartial, c.xcd_remap);
@@ -559,9 +530,16 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st) {
   const int spad = c.fspad;
-  prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo, c.d_ehi,
-                                              c.d_fDp, c.d_fG, c.d_fperm);
-  hipError_t err = hipGetLastError();
+  const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
+  const bool i8_path = spad <= 64 && fk0 >= 4 && !d_cs && !d_cells && !d_ow && c.d_B8;
+  hipError_t err;
+  if (i8_path) {
+    err = launch_prep_i8(c, batch, cap, d_pos, d_w01, fk0 == 5 ? 5 : 4, st);
+  } else {
+    prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
+                                                             c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
+    err = hipGetLastError();
+  }
   if (err != hipSuccess) return err;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
@@ -569,12 +547,18 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     e1 = c.ev_pool[c.ev_used++];
     hipEventRecord(e0, st);
   }
-  // option fact_kernel: 0 auto (pipelined for ll-only calls with S <= 64),
-  // 1 chunked, 2 pipelined with 4 waves per block, 3 pipelined with 8
-  const int fk = c.fact_kernel;
-  const bool pipe = spad <= 64 && fk != 1 && !d_cs && !d_cells && !d_ow;
+  // option fact_kernel: 0 auto (kAutoFactKernel for ll-only calls with
+  // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,
+  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves, 7 int8
+  // with the A fragments in registers
+  const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
+  const bool ll_only = !d_cs && !d_cells && !d_ow;
+  const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
+  const bool i8 = spad <= 64 && fk >= 4 && ll_only && c.d_B8;
   int np = 0;
-  if (pipe) {
+  if (i8) {
+    err = launch_score_i8(c, batch, fk == 5 ? 5 : 4, fk == 6 ? 8 : 4, fk == 7, st, &np);
+  } else if (pipe) {
     const bool w8 = fk == 3;
     switch (spad / 16) {
 #define NEMO_PIPE(NRV)                                                               \

@@ -16,6 +16,7 @@ constexpr int kMaxS = 256;         // one prep block covers all S-genes
 constexpr int kScoreWaves = 4;     // waves per score block (child split)
 constexpr int kTileCols = kWave;   // effects per score block
 constexpr int kFactWaves = 8;      // waves per factored-score block (16 effects each)
+constexpr int kI8MaxPairs = 5;     // digit-slice pairs of the int8 factored kernel
 
 // Device state of one staged model on one GPU.
 struct Ctx {
@@ -52,7 +53,9 @@ struct Ctx {
   // factored (MFMA) path: available when every off-diagonal table row is
   // shared by all children and two-valued (all tables nem.py builds)
   int score_path = 0;              // option "score_path": 0 auto, 1 stream, 2 factored
-  int fact_kernel = 0;             // option "fact_kernel": 0 auto, 1 chunked, 2/3 pipelined (4/8 waves)
+  int fact_kernel = 0;             // option "fact_kernel": 0 auto, 1 chunked, 2/3 f64 pipelined
+                                   // (4/8 waves), 4/5 int8 (4/5 digit pairs), 6 int8 x 8 waves,
+                                   // 7 int8 with A fragments in registers (1 wave/SIMD)
   bool factored = false;
   int fspad = 0;                   // S rounded up to the MFMA row-block size
   int nwords = 0;                  // 64-bit words per D1 row
@@ -64,6 +67,10 @@ struct Ctx {
   double* d_fG = nullptr;          // [cap][fspad]
   int32_t* d_fperm = nullptr;      // [cap][fspad]
   double* d_fpartial = nullptr;    // [cap][factored_partials]
+  // int8 matrix-core variant (S <= 64): fixed-point Delta digits
+  int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
+  uint8_t* d_B8 = nullptr;         // [ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
+  int8_t* d_fD8 = nullptr;         // [cap][2 * kI8MaxPairs][SPAD][64] digits
 
   // grouped (reuse) evaluation scratch
   int cap_group_batch = 0;
@@ -108,6 +115,11 @@ int pairs_per_chain(int S, int cap);
 // factored MFMA path (nemo_factored.hip)
 int factored_spad(int S);
 int factored_partials(const Ctx& c);
+// int8 matrix-core factored path (nemo_factored_i8.hip), S <= 64, ll only
+hipError_t launch_prep_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, int np,
+                          hipStream_t st);
+hipError_t launch_score_i8(Ctx& c, int batch, int np, int waves, bool areg, hipStream_t st,
+                           int* nparts);
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st);

@@ -315,8 +315,10 @@ def test_factored_detection_rejects_generic_tables():
 
 @pytest.mark.parametrize("s,e", [(2, 1), (11, 184), (16, 500), (33, 17), (40, 333), (64, 2000)])
 def test_factored_kernel_variants_agree(s, e):
-    """Chunked (fact_kernel=1) and pipelined (2: 4 waves, 3: 8 waves) factored
-    kernels against the streaming kernel and the oracle: padding rows
+    """Chunked (fact_kernel=1), f64 pipelined (2: 4 waves, 3: 8 waves) and
+    int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves,
+    7: A fragments in registers)
+    factored kernels against the streaming kernel and the oracle: padding rows
     (S % 16 != 0), ragged last tile (E % 16 != 0), tiny E; the pipelined
     kernel's bits do not depend on the batch size."""
     m = generator.synthetic_nem(s, e, 3)
@@ -331,7 +333,7 @@ def test_factored_kernel_variants_agree(s, e):
     eng.set_option("score_path", 1)
     ref = eng.score(pos, w01)
     eng.set_option("score_path", 2)
-    for fk in (1, 2, 3):
+    for fk in (1, 2, 3, 4, 5, 6, 7):
         eng.set_option("fact_kernel", fk)
         ll = eng.score(pos, w01)
         assert np.max(np.abs(ll - ref)) <= 1e-9, fk

@@ -18,10 +18,11 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        if "score_factored_kernel" in name:
-            agg["factored"].append(float(r["Counter_Value"]))
-        elif "score_kernel" in name:
-            agg["stream"].append(float(r["Counter_Value"]))
+        for tag, kind in (("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+                          ("score_factored_kernel", "factored"), ("score_kernel", "stream")):
+            if tag in name:
+                agg[kind].append(float(r["Counter_Value"]))
+                break
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
