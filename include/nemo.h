@@ -137,7 +137,7 @@ int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
  *                int8 fixed-point factored kernel, the rest the chunked fp64
  *                one; 1 = chunked; 2 / 3 = fp64 pipelined with 4 / 8 waves
  *                per block; 4 / 5 = int8 with 4 / 5 digit pairs; 6 = int8
- *                with 8 waves per block; 7 = int8, A fragments in registers
+ *                with 8 waves per block
  *   "factored"   (get only) 1 if the staged table is factorable */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);

@@ -127,7 +127,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
-                  c.d_fpartial, c.d_B8, c.d_fD8};
+                  c.d_fpartial, c.d_B8};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -158,7 +158,6 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_fG, nb * sp));
     HIPCHK(dalloc(&c.d_fperm, nb * sp));
     HIPCHK(dalloc(&c.d_fpartial, nb * (size_t)nemo::factored_partials(c)));
-    if (sp <= 64) HIPCHK(dalloc(&c.d_fD8, nb * (size_t)(2 * nemo::kI8MaxPairs) * sp * 64));
     c.cap_batch = nb;
   }
   const int nc = std::max(max_chains, 1);
@@ -563,7 +562,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 7) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..7", value);
+    if (value < 0 || value > 6) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..6", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }

@@ -320,9 +320,7 @@ __global__ void finalize_factored_kernel(int batch, int n, const double* __restr
   const int b = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
   const int lane = threadIdx.x & (kWave - 1);
   if (b >= batch) return;
-  double s = 0.0;
-  for (int t = lane; t < n; t += kWave) s += partial[(size_t)b * n + t];
-  s = fwave_sum(s);
+  const double s = sum_partials(partial + (size_t)b * n, n, lane);
   if (lane == 0) ll[b] = s;
 }
 
@@ -532,10 +530,8 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const int spad = c.fspad;
   const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool i8_path = spad <= 64 && fk0 >= 4 && !d_cs && !d_cells && !d_ow && c.d_B8;
-  hipError_t err;
-  if (i8_path) {
-    err = launch_prep_i8(c, batch, cap, d_pos, d_w01, fk0 == 5 ? 5 : 4, st);
-  } else {
+  hipError_t err = hipSuccess;
+  if (!i8_path) {  // the int8 kernel derives its Delta digits itself
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
@@ -549,15 +545,18 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   }
   // option fact_kernel: 0 auto (kAutoFactKernel for ll-only calls with
   // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,
-  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves, 7 int8
-  // with the A fragments in registers
+  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves
   const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool ll_only = !d_cs && !d_cells && !d_ow;
   const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
   const bool i8 = spad <= 64 && fk >= 4 && ll_only && c.d_B8;
   int np = 0;
+  bool finalized = false;
   if (i8) {
-    err = launch_score_i8(c, batch, fk == 5 ? 5 : 4, fk == 6 ? 8 : 4, fk == 7, st, &np);
+    // auto: 4 waves per block for large batches, 8 (fewer splits) below
+    const int waves = fk == 6 ? 8 : (fk == 4 && c.fact_kernel == 0 && batch < 384 ? 8 : 4);
+    err = launch_score_i8(c, batch, cap, d_pos, d_w01, d_ll, fk == 5 ? 5 : 4, waves, st, &np,
+                          &finalized);
   } else if (pipe) {
     const bool w8 = fk == 3;
     switch (spad / 16) {
@@ -588,7 +587,8 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     c.launches++;
   }
   // per-evaluation partials, summed in a fixed order
-  finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
+  if (!finalized)
+    finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
   return hipGetLastError();
 }
 

@@ -33,8 +33,6 @@ namespace {
 using i32x4 = __attribute__((ext_vector_type(4))) int;
 
 constexpr double kPadG8 = -1.0e6;    // G of padding rows: exp underflows to 0
-constexpr int kI8TilesPerWave = 8;   // fixed: ll bits independent of batch
-constexpr int kI8WavesPerSimd = 2;   // occupancy target of the register budget
 
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -65,6 +63,30 @@ __device__ __forceinline__ double vmax8(double a, double b) {
   return r;
 }
 
+// log(x) for finite x > 0 (normal): x = 2^k m, m in [1, 2); table entry j
+// (top 7 fraction bits) holds inv_j ~ 1/(1 + (j + 0.5)/128) and L_j =
+// -log(inv_j), so log x = k ln2 + L_j + log1p(m inv_j - 1), |m inv_j - 1| <
+// 1/254, degree-6 series.  ~1 ulp of max(|log x|, 0.5); 11 f64 + 5 integer
+// VALU against ~40 for the general log.
+__device__ __forceinline__ double log_fast(double x, const double2* __restrict__ ltab) {
+  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;  // 42 bits: k * kLn2Hi exact
+  constexpr double kLn2Lo = 5.4956039718945254e-14;
+  const uint64_t bits = __builtin_bit_cast(uint64_t, x);
+  const uint32_t hi = (uint32_t)(bits >> 32);
+  const int k = (int)((hi >> 20) & 0x7ff) - 1023;
+  const double m = __builtin_bit_cast(double, (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  const double2 tj = ltab[(hi >> 13) & 127];
+  const double r = fma(m, tj.x, -1.0);
+  double p = fma(r, -1.0 / 6.0, 0.2);
+  p = fma(r, p, -0.25);
+  p = fma(r, p, 1.0 / 3.0);
+  p = fma(r, p, -0.5);
+  p = fma(r, p, 1.0);
+  p *= r;
+  const double kd = (double)k;
+  return fma(kd, kLn2Hi, tj.y) + fma(kd, kLn2Lo, p);
+}
+
 __device__ __forceinline__ int xcd_index8(int L, int N, int remap) {
   if (!remap) return L;
   const int x = L & 7, k = L >> 3;
@@ -73,96 +95,144 @@ __device__ __forceinline__ int xcd_index8(int L, int N, int remap) {
 }
 
 // ---------------------------------------------------------------------------
-// prep: Delta digits and G in node order.  grid = batch * (SPAD / 16),
-// block = 256 (4 waves x 4 rows); lane = parent node j (SPAD <= 64).
-//   D8 [b][2NP][SPAD][64] int8,  G [b][SPAD]
+// One kernel per batch: block = (evaluation b, a range of "sets"), where set
+// s = the 8 consecutive 16-effect tiles [8s, 8s + 8).  The block first builds
+// its evaluation's Delta digits and G in LDS (node order; wave = row i, lane
+// = parent j):
+//     lo = log(1 - w + w e^lo_j), Delta = log(1 - w + w e^hi_j) - lo
+// (nem_order_mcmc.py:83-86 per factor), then every wave takes sets
+// round-robin: per tile NP pairs of i8 MFMAs per row block, exact integer
+// recombination, f64 cells, column log-sum-exp; one partial per set.
+// Partials are indexed by set, so the bits of ll do not depend on how many
+// blocks an evaluation is split into (split = f(batch), for occupancy).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void prep_i8_kernel(int S, int SPAD, int cap, int nsl, int cexp,
-                                                      const int32_t* __restrict__ pos,
-                                                      const double* __restrict__ w01,
-                                                      const double* __restrict__ e_lo,
-                                                      const double* __restrict__ e_hi,
-                                                      int8_t* __restrict__ D8, double* __restrict__ G) {
-  const int ngroups = SPAD / 16;
-  const int b = blockIdx.x / ngroups;
-  const int grp = blockIdx.x - b * ngroups;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int w = threadIdx.x / kWave;
-  const int j = lane;
-  const int* pb = pos + (size_t)b * S;
-  const int pj = j < S ? pb[j] : 0;
-  const double elo = j < S ? e_lo[j] : 1.0, ehi = j < S ? e_hi[j] : 1.0;
-  for (int i = 16 * grp + w; i < 16 * grp + 16; i += 4) {
-    double d = 0.0, lo = 0.0;
-    if (i < S && j < S) {
-      const int pi = pb[i];
-      if (pj < pi && (cap == 0 || pi - pj <= cap)) {
-        const double s = w01[((size_t)b * S + i) * S + j];
-        lo = log(fma(s, elo - 1.0, 1.0));
-        d = log(fma(s, ehi - 1.0, 1.0)) - lo;
-      }
-    }
-    const double g = wsum(lo);
-    if (lane == 0) G[(size_t)b * SPAD + i] = i < S ? g : kPadG8;
-    // fixed-point digits: x = Delta * 2^(6-c) in [-32, 32]; each step is exact
-    double x = ldexp(d, 6 - cexp);
-    int8_t* out = D8 + (((size_t)b * nsl) * SPAD + i) * 64 + j;
-    for (int s = 0; s < nsl; ++s) {
-      const double q = rint(x);
-      out[(size_t)s * SPAD * 64] = (int8_t)(int)q;
-      x = (x - q) * 64.0;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// score: block = (evaluation b, WAVES * 8 consecutive 16-effect tiles),
-// wave = tiles t_begin + w, + WAVES, ...; grid = batch * split (XCD remap,
-// evaluation-major).  Every wave: per tile, NP pairs of i8 MFMAs per row
-// block, exact integer recombination, f64 cells, column log-sum-exp.
-// ---------------------------------------------------------------------------
-template <int NR, int WAVES, int NP, bool AREG>
-__global__ __launch_bounds__(WAVES * kWave, AREG ? 1 : kI8WavesPerSimd) void score_i8_kernel(
-    int S, int E, int ntiles, int split, const int8_t* __restrict__ D8,
-    const double* __restrict__ Gd, const uint8_t* __restrict__ B8, const double* __restrict__ U,
-    double sA, double sB, double sC, double* __restrict__ partial, int remap) {
+template <int NR, int WAVES, int NP>
+__global__ __launch_bounds__(WAVES * kWave, 2) void score_i8_kernel(
+    int S, int E, int ntiles, int nsets, int split, int cap, int cexp,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const double* __restrict__ U, double sA, double sB,
+    double sC, double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
   constexpr int SPAD = NR * 16;
   constexpr int NSL = 2 * NP;
   extern __shared__ __attribute__((aligned(16))) double lds8[];
-  double* etab = lds8;                                   // [256]
-  double* Gs = etab + 256;                               // [SPAD]
-  i32x4* A = (i32x4*)(Gs + SPAD);                        // [NSL][SPAD][5] 16-byte chunks
-                                                         // (80-B rows: conflict-free b128)
+  double* etab = lds8;                                   // [256] 2^(j/256)
+  double2* ltab = (double2*)(etab + 256);                // [128] log table
+  double* Gs = (double*)(ltab + 128);                    // [SPAD]
+  double* elo_s = Gs + SPAD;                             // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  int* perm_s = (int*)(ehi_s + SPAD);                    // [SPAD] node at each position
+  i32x4* A = (i32x4*)(perm_s + SPAD);                    // [NSL][SPAD][5] 16-byte chunks
+  int8_t* A8 = (int8_t*)A;                               // (80-B rows: conflict-free b128)
 
   const int work = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
   const int b = work / split;
   const int part = work - b * split;
-  const int t_begin = part * kI8TilesPerWave * WAVES;
-  const int t_end = min(ntiles, t_begin + kI8TilesPerWave * WAVES);
+  const int spb = (nsets + split - 1) / split;
+  const int s_begin = part * spb;
+  const int s_end = min(nsets, s_begin + spb);
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int col = lane & 15, rg = lane >> 4;
 
   for (int k = tid; k < 256; k += blockDim.x) etab[k] = exp2((double)k * (1.0 / 256.0));
-  for (int k = tid; k < SPAD; k += blockDim.x) Gs[k] = Gd[(size_t)b * SPAD + k];
-  const i32x4* Ag = (const i32x4*)(D8 + (size_t)b * NSL * SPAD * 64);
-  for (int k = tid; k < NSL * SPAD * 4; k += blockDim.x) A[(k >> 2) * 5 + (k & 3)] = Ag[k];
+  for (int k = tid; k < 128; k += blockDim.x) {
+    const double inv = 1.0 / (1.0 + ((double)k + 0.5) * (1.0 / 128.0));
+    ltab[k] = double2{inv, -log(inv)};
+  }
+  {
+    const int32_t* pb = pos + (size_t)b * S;
+    for (int j = tid; j < S; j += blockDim.x) {
+      int pj = pb[j];
+      pj = pj < 0 ? 0 : (pj >= S ? S - 1 : pj);  // malformed input must not fault
+      perm_s[pj] = j;
+    }
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      Gs[i] = i < S ? 0.0 : kPadG8;
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+    i32x4* a4 = A;
+    for (int k = tid; k < NSL * SPAD * 5; k += blockDim.x) a4[k] = i32x4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  // ---- Delta digits and G of evaluation b.  Work runs in ORDER positions:
+  // the child at position q has the parents at positions < q (within `cap`),
+  // so pass q packs the children at positions q and S-1-q into one wave --
+  // lane p < q: (q, p); lane p >= q: (S-1-q, p-q) -- every lane one
+  // (child, parent) pair.  Digits land at [child node][parent node].
+  {
+    const bool packed = cap == 0 || cap >= S - 1;
+    const int npass = packed ? (S + 1) / 2 : S;
+    const int p = lane;
+    // this wave's passes q = w, w + WAVES, ... (at most kMaxPass): the
+    // (child, parent) pair of every lane and its weight are fetched first,
+    // so the global loads of all passes are in flight together
+    constexpr int kMaxPass = (SPAD / 2 + WAVES - 1) / WAVES + (SPAD % 2);
+    constexpr int kMaxPassAll = (SPAD + WAVES - 1) / WAVES;
+    int ii[kMaxPassAll], jj[kMaxPassAll];
+    double sw[kMaxPassAll];
+#pragma unroll
+    for (int k = 0; k < kMaxPassAll; ++k) {
+      const int q = w + k * WAVES;
+      int qr = 0, pp = 0;
+      bool act = false;
+      if (q < npass) {
+        if (packed) {
+          const int q2 = S - 1 - q;
+          if (p < q) { qr = q; pp = p; act = true; }
+          else { qr = q2; pp = p - q; act = q2 != q && pp < q2; }
+        } else {
+          const int np = q < cap ? q : cap;
+          qr = q; pp = q - 1 - p; act = p < np;
+        }
+      }
+      ii[k] = act ? perm_s[qr] : -1;
+      jj[k] = act ? perm_s[pp] : 0;
+      sw[k] = act ? w01[((size_t)b * S + ii[k]) * S + jj[k]] : 0.0;
+    }
+    (void)kMaxPass;
+#pragma unroll
+    for (int k = 0; k < kMaxPassAll; ++k) {
+      const int q = w + k * WAVES;
+      if (q >= npass) break;
+      const bool act = ii[k] >= 0;
+      double lo = 0.0;
+      if (act) {
+        const int i = ii[k], j = jj[k];
+        lo = log_fast(fma(sw[k], elo_s[j] - 1.0, 1.0), ltab);
+        const double d = log_fast(fma(sw[k], ehi_s[j] - 1.0, 1.0), ltab) - lo;
+        // fixed point: x = Delta * 2^(6-c) in [-32, 32]; every step is exact
+        double x = ldexp(d, 6 - cexp);
+#pragma unroll
+        for (int sl = 0; sl < NSL; ++sl) {
+          const double qd = rint(x);
+          A8[(sl * SPAD + i) * 80 + j] = (int8_t)(int)qd;
+          x = (x - qd) * 64.0;
+        }
+      }
+      // G of the one or two children of this pass (segmented wave sums)
+      const double ga = wsum((act && p < q) || !packed ? lo : 0.0);
+      if (packed) {
+        const double gb = wsum(act && p >= q ? lo : 0.0);
+        if (lane == 0 && S - 1 - q != q) Gs[perm_s[S - 1 - q]] = gb;
+      }
+      if (lane == 0) Gs[perm_s[q]] = ga;
+    }
+  }
   // U rows of this lane's cells: 16r + 4rg + g (i8 C layout).  The staged U
   // has >= SPAD rows (rows S+1.. are zero; their G is kPadG8), so a cell's
-  // address is a uniform part ((16r + g) E, an SGPR base) + one per-lane
-  // offset (4 rg E + col): no per-load VALU.
+  // address is a uniform part ((16r + g) E) + one per-lane offset (4 rg E + col).
   const uint32_t uln = (uint32_t)(4 * rg * E + col);
   __syncthreads();
 
-  double* part_out = partial + (size_t)b * split * WAVES + part * WAVES + w;
-  int t = t_begin + w;
-  if (t >= t_end) {
-    if (lane == 0) *part_out = 0.0;
-    return;
-  }
   const i32x4* Bt = (const i32x4*)B8;
-
+  const uint32_t a_lane = (uint32_t)(col * 5 + rg);  // A chunk of this lane, row block 0, slice 0
+  // one flat stream of (set, tile) per wave, so the next tile's U rows and
+  // D1 bytes are always in flight -- across set boundaries too
+  int set = s_begin + w;
+  if (set < s_end) {
   double msum = 0.0, lprod = 1.0;
   int lexp = 0;
   double uc[NR][4], unc;
@@ -176,13 +246,13 @@ __global__ __launch_bounds__(WAVES * kWave, AREG ? 1 : kI8WavesPerSimd) void sco
     unc = (base + (size_t)S * E)[col];
     bc = Bt[(size_t)tt * kWave + lane];
   };
+  int t = 8 * set;
   load_tile(t);
-  const uint32_t a_lane = (uint32_t)(col * 5 + rg);  // A chunk of this lane, row block 0, slice 0
-  for (; t < t_end; t += WAVES) {
+  for (;;) {
     // launder the A offset each tile: keeps the loop-invariant A fragments
     // (2NP * NR * 16 B per lane) in LDS instead of hoisted into registers
     uint32_t ao = a_lane;
-    if constexpr (!AREG) asm volatile("" : "+v"(ao));
+    asm volatile("" : "+v"(ao));
     const i32x4* Al = A + ao;
     const i32x4 b1 = bc;
     const i32x4 b64 = b1 << 6;  // bytes 0/1 -> 0/64
@@ -209,7 +279,14 @@ __global__ __launch_bounds__(WAVES * kWave, AREG ? 1 : kI8WavesPerSimd) void sco
       }
     }
     const double unull = unc;
-    if (t + WAVES < t_end) load_tile(t + WAVES);
+    // next (set, tile) of this wave
+    int tn = t + 1, setn = set;
+    if (tn >= min(ntiles, 8 * set + 8)) {
+      setn = set + WAVES;
+      tn = 8 * setn;
+    }
+    const bool more = setn < s_end;
+    if (more) load_tile(tn);
     // column log-sum-exp over the SPAD rows and the null row
     const bool valid = t * 16 + col < E;
     double m = unull;
@@ -227,54 +304,71 @@ __global__ __launch_bounds__(WAVES * kWave, AREG ? 1 : kI8WavesPerSimd) void sco
     l += __shfl_xor(l, 16, kWave);
     l += __shfl_xor(l, 32, kWave);
     l += exp_lse8(unull - m, etab);
+    // prod(l) kept as mantissa * 2^lexp: branch-free, no overflow
     msum += valid ? m : 0.0;
     lprod *= valid ? l : 1.0;
     lexp += __builtin_amdgcn_frexp_exp(lprod);
     lprod = __builtin_amdgcn_frexp_mant(lprod);
+    if (setn != set) {  // set complete: one partial
+      double v = msum + (log(lprod) + (double)lexp * 0.69314718055994530942);
+      v = lane < 16 ? v : 0.0;
+      v = wsum(v);
+      if (lane == 0) partial[(size_t)b * nsets + set] = v;
+      msum = 0.0;
+      lprod = 1.0;
+      lexp = 0;
+    }
+    if (!more) break;
+    t = tn;
+    set = setn;
   }
-  double v = msum + (log(lprod) + (double)lexp * 0.69314718055994530942);
-  v = lane < 16 ? v : 0.0;
-  v = wsum(v);
-  if (lane == 0) *part_out = v;
+  }
+  // ---- one block per evaluation: it sums its own partials (same order as
+  // finalize_factored_kernel, so the bits match the split > 1 path)
+  if (split == 1) {
+    __syncthreads();  // the block's partial stores are visible to the block
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nsets, nsets, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
 }
 
-template <int NR, int WAVES, int NP, bool AREG>
-hipError_t launch_i8_t(Ctx& c, int batch, hipStream_t st, int* nparts) {
+template <int NR, int WAVES, int NP>
+hipError_t launch_i8_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                       double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
   const int ntiles = (c.E + 15) / 16;
-  const int tpb = kI8TilesPerWave * WAVES;
-  const int split = (ntiles + tpb - 1) / tpb;
-  const size_t lds = 256 * 8 + SPAD * 8 + (size_t)2 * NP * SPAD * 80;
+  const int nsets = (ntiles + 7) / 8;
+  // blocks per evaluation: fill 2 waves per SIMD on 256 CUs; each split
+  // re-derives its evaluation's digits (cheap next to its tiles)
+  const int slots = 256 * (8 / WAVES);
+  int split = (slots + batch - 1) / batch;
+  split = split < 1 ? 1 : (split > nsets ? nsets : split);
+  const size_t lds = 256 * 8 + 128 * 16 + 3 * SPAD * 8 + SPAD * 4 + (size_t)2 * NP * SPAD * 80;
   const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48),
                sC = ldexp(1.0, c.i8_cexp - 60);
-  score_i8_kernel<NR, WAVES, NP, AREG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
-      c.S, c.E, ntiles, split, c.d_fD8, c.d_fG, c.d_B8, (const double*)c.d_U64, sA, sB, sC,
-      c.d_fpartial, c.xcd_remap);
-  *nparts = split * WAVES;
+  score_i8_kernel<NR, WAVES, NP><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+      (const double*)c.d_U64, sA, sB, sC, c.d_fpartial, d_ll, c.xcd_remap);
+  *nparts = nsets;
+  *finalized = split == 1;
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_prep_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, int np,
-                          hipStream_t st) {
-  const int spad = c.fspad;
-  if (spad > 64 || np < 4 || np > kI8MaxPairs) return hipErrorInvalidValue;
-  prep_i8_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, 2 * np, c.i8_cexp, d_pos, d_w01,
-                                                     c.d_elo, c.d_ehi, c.d_fD8, c.d_fG);
-  return hipGetLastError();
-}
-
-hipError_t launch_score_i8(Ctx& c, int batch, int np, int waves, bool areg, hipStream_t st,
-                           int* nparts) {
+hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                           double* d_ll, int np, int waves, hipStream_t st, int* nparts,
+                           bool* finalized) {
   const int nr = c.fspad / 16;
-#define NEMO_I8(NRV, WV, NPV, AR)                           \
-  if (nr == NRV && waves == WV && np == NPV && areg == AR) \
-    return launch_i8_t<NRV, WV, NPV, AR>(c, batch, st, nparts);
-  NEMO_I8(1, 4, 4, false) NEMO_I8(2, 4, 4, false) NEMO_I8(4, 4, 4, false)
-  NEMO_I8(1, 4, 5, false) NEMO_I8(2, 4, 5, false) NEMO_I8(4, 4, 5, false)
-  NEMO_I8(1, 8, 4, false) NEMO_I8(2, 8, 4, false) NEMO_I8(4, 8, 4, false)
-  NEMO_I8(1, 4, 4, true) NEMO_I8(2, 4, 4, true) NEMO_I8(4, 4, 4, true)
+  if (c.fspad > 64 || !c.d_B8) return hipErrorInvalidValue;
+#define NEMO_I8(NRV, WV, NPV) \
+  if (nr == NRV && waves == WV && np == NPV) \
+    return launch_i8_t<NRV, WV, NPV>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized);
+  NEMO_I8(1, 4, 4) NEMO_I8(2, 4, 4) NEMO_I8(4, 4, 4)
+  NEMO_I8(1, 4, 5) NEMO_I8(2, 4, 5) NEMO_I8(4, 4, 5)
+  NEMO_I8(1, 8, 4) NEMO_I8(2, 8, 4) NEMO_I8(4, 8, 4)
 #undef NEMO_I8
   return hipErrorInvalidValue;
 }

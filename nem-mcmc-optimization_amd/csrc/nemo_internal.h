@@ -54,8 +54,7 @@ struct Ctx {
   // shared by all children and two-valued (all tables nem.py builds)
   int score_path = 0;              // option "score_path": 0 auto, 1 stream, 2 factored
   int fact_kernel = 0;             // option "fact_kernel": 0 auto, 1 chunked, 2/3 f64 pipelined
-                                   // (4/8 waves), 4/5 int8 (4/5 digit pairs), 6 int8 x 8 waves,
-                                   // 7 int8 with A fragments in registers (1 wave/SIMD)
+                                   // (4/8 waves), 4/5 int8 (4/5 digit pairs), 6 int8 x 8 waves
   bool factored = false;
   int fspad = 0;                   // S rounded up to the MFMA row-block size
   int nwords = 0;                  // 64-bit words per D1 row
@@ -70,7 +69,6 @@ struct Ctx {
   // int8 matrix-core variant (S <= 64): fixed-point Delta digits
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
   uint8_t* d_B8 = nullptr;         // [ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
-  int8_t* d_fD8 = nullptr;         // [cap][2 * kI8MaxPairs][SPAD][64] digits
 
   // grouped (reuse) evaluation scratch
   int cap_group_batch = 0;
@@ -115,11 +113,24 @@ int pairs_per_chain(int S, int cap);
 // factored MFMA path (nemo_factored.hip)
 int factored_spad(int S);
 int factored_partials(const Ctx& c);
-// int8 matrix-core factored path (nemo_factored_i8.hip), S <= 64, ll only
-hipError_t launch_prep_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, int np,
-                          hipStream_t st);
-hipError_t launch_score_i8(Ctx& c, int batch, int np, int waves, bool areg, hipStream_t st,
-                           int* nparts);
+// int8 matrix-core factored path (nemo_factored_i8.hip), S <= 64, ll only:
+// one kernel (digits of Delta built in LDS + score); partials per 8-tile set
+// (*finalized: ll already written -- one block per evaluation -- else the
+// caller sums the nparts partials per evaluation with sum_partials' order)
+hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                           double* d_ll, int np, int waves, hipStream_t st, int* nparts,
+                           bool* finalized);
+
+// fixed-order sum of n partials by one wave: strided lane sums, then an xor
+// tree (finalize_factored_kernel and the int8 kernel's own finalize share it,
+// so both paths give identical bits)
+__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int n, int lane) {
+  double s = 0.0;
+  for (int t = lane; t < n; t += kWave) s += p[t];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, kWave);
+  return s;
+}
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st);

@@ -316,8 +316,7 @@ def test_factored_detection_rejects_generic_tables():
 @pytest.mark.parametrize("s,e", [(2, 1), (11, 184), (16, 500), (33, 17), (40, 333), (64, 2000)])
 def test_factored_kernel_variants_agree(s, e):
     """Chunked (fact_kernel=1), f64 pipelined (2: 4 waves, 3: 8 waves) and
-    int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves,
-    7: A fragments in registers)
+    int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves)
     factored kernels against the streaming kernel and the oracle: padding rows
     (S % 16 != 0), ragged last tile (E % 16 != 0), tiny E; the pipelined
     kernel's bits do not depend on the batch size."""
@@ -330,15 +329,17 @@ def test_factored_kernel_variants_agree(s, e):
     perms = [rng.permutation(s) for _ in range(b)]
     pos = np.array([_pos(p) for p in perms])
     w01 = expit(rng.uniform(-4, 4, (b, s, s)))
-    eng.set_option("score_path", 1)
-    ref = eng.score(pos, w01)
-    eng.set_option("score_path", 2)
-    for fk in (1, 2, 3, 4, 5, 6, 7):
-        eng.set_option("fact_kernel", fk)
-        ll = eng.score(pos, w01)
-        assert np.max(np.abs(ll - ref)) <= 1e-9, fk
-        for c in (0, 11, 36):
-            assert eng.score(pos[c:c + 1], w01[c:c + 1])[0] == ll[c]
+    for cap in (0, 5):
+        eng.set_option("score_path", 1)
+        ref = eng.score(pos, w01, cap=cap)
+        eng.set_option("score_path", 2)
+        for fk in (1, 2, 3, 4, 5, 6):
+            eng.set_option("fact_kernel", fk)
+            ll = eng.score(pos, w01, cap=cap)
+            assert np.max(np.abs(ll - ref)) <= 1e-9, (fk, cap)
+            for c in (0, 11, 36):
+                assert eng.score(pos[c:c + 1], w01[c:c + 1], cap=cap)[0] == ll[c], (fk, cap)
+    ll = eng.score(pos, w01)
     for c in (0, 1):
         assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-9
     # zero and one weights (G, Delta at their extremes)
@@ -350,3 +351,22 @@ def test_factored_kernel_variants_agree(s, e):
         assert np.max(np.abs(a - eng.score(pos[:2], wz))) <= 1e-9
         eng.set_option("score_path", 2)
     eng.close()
+
+
+def test_int8_kernel_bits_independent_of_split(c3_model):
+    """The int8 kernel splits an evaluation over more blocks for small batches
+    (and sums its partials in-kernel when one block owns it); ll bits must not
+    depend on the batch size."""
+    m, eng = c3_model
+    s = m.num_s
+    rng = np.random.default_rng(21)
+    b = 300
+    pos = np.array([rng.permutation(s) for _ in range(b)], dtype=np.int32)
+    w01 = expit(rng.uniform(-3, 3, (b, s, s)))
+    eng.set_option("fact_kernel", 0)
+    big = eng.score(pos, w01)
+    for n in (1, 5, 64):
+        assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
+    eng.set_option("score_path", 1)
+    assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-9
+    eng.set_option("score_path", 0)
