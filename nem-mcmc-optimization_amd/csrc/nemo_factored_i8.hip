@@ -9,7 +9,7 @@
 // written in fixed point against one per-model scale 2^c >= 2 max|hi - lo|
 // (|Delta(i,j)| <= |hi_j - lo_j| for every weight):
 //     Delta = 2^(c-6) * sum_{s<2NP} d_s * 64^-s,   d_s integers in [-32, 32],
-// error <= 2^(c-6-6*2NP-1) per entry (NP = 4: 2^-45 at c = 4).  Each pair of
+// error <= 2^(c-6) 64^-(2NP-1) / 2 per entry (NP = 4: 2^(c-49), 2^-45 at c = 4).  Each pair of
 // digit slices is one integer accumulation on v_mfma_i32_16x16x64_i8 (K = 64
 // parents in one instruction): the first MFMA takes d_2t against B = 64*D1,
 // the second d_2t+1 against B = D1 into the same accumulator, so
@@ -63,30 +63,6 @@ __device__ __forceinline__ double vmax8(double a, double b) {
   return r;
 }
 
-// log(x) for finite x > 0 (normal): x = 2^k m, m in [1, 2); table entry j
-// (top 7 fraction bits) holds inv_j ~ 1/(1 + (j + 0.5)/128) and L_j =
-// -log(inv_j), so log x = k ln2 + L_j + log1p(m inv_j - 1), |m inv_j - 1| <
-// 1/254, degree-6 series.  ~1 ulp of max(|log x|, 0.5); 11 f64 + 5 integer
-// VALU against ~40 for the general log.
-__device__ __forceinline__ double log_fast(double x, const double2* __restrict__ ltab) {
-  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;  // 42 bits: k * kLn2Hi exact
-  constexpr double kLn2Lo = 5.4956039718945254e-14;
-  const uint64_t bits = __builtin_bit_cast(uint64_t, x);
-  const uint32_t hi = (uint32_t)(bits >> 32);
-  const int k = (int)((hi >> 20) & 0x7ff) - 1023;
-  const double m = __builtin_bit_cast(double, (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-  const double2 tj = ltab[(hi >> 13) & 127];
-  const double r = fma(m, tj.x, -1.0);
-  double p = fma(r, -1.0 / 6.0, 0.2);
-  p = fma(r, p, -0.25);
-  p = fma(r, p, 1.0 / 3.0);
-  p = fma(r, p, -0.5);
-  p = fma(r, p, 1.0);
-  p *= r;
-  const double kd = (double)k;
-  return fma(kd, kLn2Hi, tj.y) + fma(kd, kLn2Lo, p);
-}
-
 __device__ __forceinline__ int xcd_index8(int L, int N, int remap) {
   if (!remap) return L;
   const int x = L & 7, k = L >> 3;
@@ -137,10 +113,7 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_i8_kernel(
   const int col = lane & 15, rg = lane >> 4;
 
   for (int k = tid; k < 256; k += blockDim.x) etab[k] = exp2((double)k * (1.0 / 256.0));
-  for (int k = tid; k < 128; k += blockDim.x) {
-    const double inv = 1.0 / (1.0 + ((double)k + 0.5) * (1.0 / 128.0));
-    ltab[k] = double2{inv, -log(inv)};
-  }
+  fill_log_table(ltab, tid, blockDim.x);
   {
     const int32_t* pb = pos + (size_t)b * S;
     for (int j = tid; j < S; j += blockDim.x) {

@@ -121,6 +121,39 @@ hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, con
                            double* d_ll, int np, int waves, hipStream_t st, int* nparts,
                            bool* finalized);
 
+// log(x) for finite x > 0 (normal): x = 2^k m, m in [1, 2); table entry j
+// (top 7 fraction bits) holds inv_j ~ 1/(1 + (j + 0.5)/128) and L_j =
+// -log(inv_j), so log x = k ln2 + L_j + log1p(m inv_j - 1), |m inv_j - 1| <
+// 1/254, degree-6 series.  Within ~1 ulp of max(|log x|, 0.5) (restated and
+// checked against a 120-bit reference in tests/test_numerics.py); 11 f64 + 5
+// integer VALU and one LDS read, against ~45 VALU for the general log.
+__device__ __forceinline__ double log_fast(double x, const double2* __restrict__ ltab) {
+  constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;  // 42 bits: k * kLn2Hi exact
+  constexpr double kLn2Lo = 5.4956039718945254e-14;
+  const uint64_t bits = __builtin_bit_cast(uint64_t, x);
+  const uint32_t hi = (uint32_t)(bits >> 32);
+  const int k = (int)((hi >> 20) & 0x7ff) - 1023;
+  const double m = __builtin_bit_cast(double, (bits & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  const double2 tj = ltab[(hi >> 13) & 127];
+  const double r = fma(m, tj.x, -1.0);
+  double p = fma(r, -1.0 / 6.0, 0.2);
+  p = fma(r, p, -0.25);
+  p = fma(r, p, 1.0 / 3.0);
+  p = fma(r, p, -0.5);
+  p = fma(r, p, 1.0);
+  p *= r;
+  const double kd = (double)k;
+  return fma(kd, kLn2Hi, tj.y) + fma(kd, kLn2Lo, p);
+}
+
+// the 128-entry table of log_fast (2 KB of LDS), filled by a block
+__device__ __forceinline__ void fill_log_table(double2* ltab, int tid, int nthreads) {
+  for (int k = tid; k < 128; k += nthreads) {
+    const double inv = 1.0 / (1.0 + ((double)k + 0.5) * (1.0 / 128.0));
+    ltab[k] = double2{inv, -log(inv)};
+  }
+}
+
 // fixed-order sum of n partials by one wave: strided lane sums, then an xor
 // tree (finalize_factored_kernel and the int8 kernel's own finalize share it,
 // so both paths give identical bits)

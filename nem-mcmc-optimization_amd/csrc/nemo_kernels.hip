@@ -395,6 +395,7 @@ template <int NPL>
 struct LocalObjective {
   double c[NPL];  // this lane's share of the c vector, kept in registers
   double anc;
+  const double2* ltab;  // log_fast table (LDS)
   __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
 #pragma clang fp contract(off)
     const double e0 = expit_d(x0);
@@ -402,8 +403,8 @@ struct LocalObjective {
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
     for (int q = 0; q < NPL; ++q) {
-      p0 += log(c[q] * e0 + 1.0);
-      p1 += log(c[q] * e1 + 1.0);
+      p0 += log_fast(c[q] * e0 + 1.0, ltab);
+      p1 += log_fast(c[q] * e1 + 1.0, ltab);
     }
     p0 = wave_sum(p0);
     p1 = wave_sum(p1);
@@ -427,6 +428,9 @@ __global__ __launch_bounds__(256) void local_opt_pairs_kernel(
     const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
     double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
     int32_t* __restrict__ info) {
+  __shared__ double2 ltab[128];
+  fill_log_table(ltab, threadIdx.x, blockDim.x);
+  __syncthreads();
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (gw >= nchains * npairs) return;  // uniform per wave
@@ -441,6 +445,7 @@ __global__ __launch_bounds__(256) void local_opt_pairs_kernel(
   const TT* tv = eT + ((size_t)i * S + k) * E;
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   LocalObjective<NPL> obj;
+  obj.ltab = ltab;
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
     const int e = q * kWave + lane;
@@ -461,10 +466,14 @@ template <int NPL>
 __global__ __launch_bounds__(256) void local_opt_generic_kernel(
     int n, int E, const double* __restrict__ cvec, const double* __restrict__ anc,
     const double* __restrict__ x0, double* __restrict__ out) {
+  __shared__ double2 ltab[128];
+  fill_log_table(ltab, threadIdx.x, blockDim.x);
+  __syncthreads();
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (gw >= n) return;
   LocalObjective<NPL> obj;
+  obj.ltab = ltab;
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
     const int e = q * kWave + lane;
