@@ -28,6 +28,99 @@ def shard(n_chains: int, rank: int, world: int) -> range:
     return range(start, start + base + (1 if rank < extra else 0))
 
 
+def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0):
+    """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
+    chain in ONE fused device call; each chain's state is updated exactly as
+    its own call would (same kernels, batch-invariant bits)."""
+    s = chains[0].num_s
+    pos = np.stack([c._pos for c in chains]).astype(np.int32)
+    w = np.stack([c.parent_weights for c in chains])
+    w01 = expit(w)
+    anc = np.empty_like(w)
+    eye = np.identity(s)
+    for k, c in enumerate(chains):
+        c.ll = 0.0
+        c.ancestor_x = np.clip(inv(eye - c.expit_parent_weights(w[k])) - eye, 0, 1)
+        anc[k] = c.ancestor_x
+    w_new, ll1, lld, _ = engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
+    out = np.empty(len(chains))
+    for k, c in enumerate(chains):
+        c._eval1 = (pos[k].copy(), w01[k].copy())
+        c.parent_weights = w_new[k].copy()
+        c.ll = float(ll1[k])
+        if use_nem:
+            _, dag = c.create_nem(c.parent_weights)
+            out[k] = float(engine.score(c._pos[None, :], expit(dag.astype(float))[None], cap=cap)[0])
+        else:
+            out[k] = float(lld[k])
+    return out
+
+
+def opt_weights_batch(chains, engine: Engine, cap=0):
+    """The documented ``opt_weights`` pass-through of every
+    chain in one batched score call: the score of its binarised weights."""
+    pos = np.stack([c._pos for c in chains]).astype(np.int32)
+    w01d = np.stack([expit(np.asarray(c.create_dag(c.parent_weights)[1], dtype=np.float64))
+                     for c in chains])
+    ll = engine.score(pos, w01d, cap=cap)
+    for k, c in enumerate(chains):
+        c.ll = float(ll[k])
+    return np.asarray(ll, dtype=np.float64)
+
+
+def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0):
+    """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
+    lock-step: each MCMC step is one ``optimal_weights_batch`` call.  Chain k
+    draws from ``chains[k].rng`` in the reference's call order, and ends with
+    the attributes its own ``method`` call would leave (best_score, best_dag,
+    best_order, score lists, parents_list of the best order).  Returns the
+    per-chain best scores."""
+    n = len(chains)
+    s = chains[0].num_s
+    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap)
+    curr = list(opt_weights_batch(chains, engine, cap=cap))
+    st = []
+    for k, c in enumerate(chains):
+        dag, _ = c.create_dag(c.parent_weights)
+        st.append(dict(best=curr[k], best_dag=dag, curr_perm=c.perm_order, best_order=c.perm_order,
+                       best_order_list=[c.perm_order], curr_dag=np.zeros((s, s)),
+                       curr_list=[curr[k]], best_list=[curr[k]], all_list=[curr[k]],
+                       best_parents=c.parents_list.copy(), best_struct=(c._pos, c._mask), acc=[]))
+    for _ in range(n_iterations):
+        props = []
+        for k, c in enumerate(chains):
+            perm, i1, i2 = c.get_new_order(st[k]["curr_perm"], swap_prob=swap_prob)
+            c.reset(perm_order=perm, i1=i1, i2=i2)
+            props.append(perm)
+        lls = optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap)
+        for k, c in enumerate(chains):
+            q = st[k]
+            ll = float(lls[k])
+            q["all_list"].append(ll)
+            dag = c.create_nem(c.parent_weights)[0] if use_nem else c.create_dag(c.parent_weights)[0]
+            q["curr_list"].append(curr[k])
+            acc, curr[k], q["curr_dag"], q["curr_perm"] = c.accepting(
+                ll, curr[k], gammas[k], dag, q["curr_dag"], props[k], q["curr_perm"])
+            q["acc"].append(acc)
+            if acc and curr[k] > q["best"]:
+                q["best"] = curr[k]
+                q["best_dag"] = dag
+                q["best_order"] = q["curr_perm"].copy()
+                q["best_parents"] = c.parents_list.copy()
+                q["best_struct"] = (c._pos, c._mask)
+                q["best_list"].append(q["best"])
+                q["best_order_list"].append(q["best_order"])
+    for k, c in enumerate(chains):
+        q = st[k]
+        c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]
+        c.all_score_list, c.curr_score_list = q["all_list"], q["curr_list"]
+        c.best_score_list, c.best_order_list = q["best_list"], q["best_order_list"]
+        c.accepted = q["acc"]
+        c.parents_list = q["best_parents"]
+        c._pos, c._mask = q["best_struct"]
+    return np.array([q["best"] for q in st])
+
+
 class ChainBatch:
     """``n`` independent order-MCMC chains on one staged model.
 
@@ -53,53 +146,14 @@ class ChainBatch:
             self.chains.append(c)
         self.engine.reserve(self.n, self.n)
 
-    # one batched get_optimal_weights(init=True) over all chains
-    def _optimal_weights(self):
-        s = self.nem.num_s
-        pos = np.stack([c._pos for c in self.chains]).astype(np.int32)
-        w = np.stack([c.parent_weights for c in self.chains])
-        w01 = expit(w)
-        anc = np.empty_like(w)
-        eye = np.identity(s)
-        for k, c in enumerate(self.chains):
-            c.ancestor_x = np.clip(inv(eye - c.expit_parent_weights(w[k])) - eye, 0, 1)
-            anc[k] = c.ancestor_x
-        w_new, ll1, lld, _ = self.engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=self.cap)
-        out = np.empty(self.n)
-        for k, c in enumerate(self.chains):
-            c.parent_weights = w_new[k].copy()
-            c.ll = float(ll1[k])
-            if self.use_nem:
-                _, dag = c.create_nem(c.parent_weights)
-                out[k] = float(self.engine.score(c._pos[None, :], expit(dag.astype(float))[None],
-                                                 cap=self.cap)[0])
-            else:
-                out[k] = float(lld[k])
-        return out
-
     def run(self, n_iterations: int):
         """Every chain runs the reference's ``method`` loop
-        (nem_order_mcmc.py:257-310) for ``n_iterations`` steps."""
-        curr = self._optimal_weights()
-        self.curr_scores = curr.copy()
-        self.best_scores = curr.copy()
-        self.curr_orders = [c.perm_order for c in self.chains]
-        self.best_orders = [np.asarray(o).copy() for o in self.curr_orders]
-        self.accepted = np.zeros((n_iterations, self.n), dtype=bool)
-        for it in range(n_iterations):
-            props = []
-            for k, c in enumerate(self.chains):
-                perm, i1, i2 = c.get_new_order(self.curr_orders[k], swap_prob=self.swap_prob)
-                c.reset(perm_order=perm, i1=i1, i2=i2)
-                props.append(perm)
-            lls = self._optimal_weights()
-            for k, c in enumerate(self.chains):
-                acc, self.curr_scores[k], _, self.curr_orders[k] = c.accepting(
-                    lls[k], self.curr_scores[k], self.gammas[k], None, None, props[k], self.curr_orders[k])
-                self.accepted[it, k] = acc
-                if acc and self.curr_scores[k] > self.best_scores[k]:
-                    self.best_scores[k] = self.curr_scores[k]
-                    self.best_orders[k] = np.asarray(self.curr_orders[k]).copy()
+        (nem_order_mcmc.py:257-310) for ``n_iterations`` steps.  Returns
+        (best scores [n], best orders [n, S])."""
+        self.best_scores = run_methods(self.chains, self.gammas, n_iterations, self.engine,
+                                       swap_prob=self.swap_prob, use_nem=self.use_nem, cap=self.cap)
+        self.best_orders = [np.asarray(c.best_order).copy() for c in self.chains]
+        self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(n_iterations, self.n)
         return self.best_scores, np.stack(self.best_orders)
 
 

@@ -273,6 +273,7 @@ class NEMOrderMCMC:
         best_score_list = [best_score]
         all_score_list = [curr_score]
         best_parents_list = self.parents_list.copy()
+        best_struct = (self._pos, self._mask)   # the device mask behind parents_list
         accepted = []
         for it in range(n_iterations):
             if verbose and it % 50 == 0:
@@ -295,6 +296,7 @@ class NEMOrderMCMC:
                 best_dag = dag
                 best_order = curr_perm_order.copy()
                 best_parents_list = self.parents_list.copy()
+                best_struct = (self._pos, self._mask)
                 best_score_list.append(best_score)
                 best_order_list.append(best_order)
         self.best_score = best_score
@@ -305,7 +307,11 @@ class NEMOrderMCMC:
         self.best_score_list = best_score_list
         self.best_order_list = best_order_list
         self.accepted = accepted
+        # the reference leaves parents_list at the best order's parent sets
+        # (n_parents stays stale, as there); the next method() call -- replica
+        # exchange rounds -- scores with them
         self.parents_list = best_parents_list
+        self._pos, self._mask = best_struct
         return best_score, best_dag
 
     def condition(self, i, j):

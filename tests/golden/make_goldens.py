@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -189,9 +189,48 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
         print(f"localopt_{name}: {len(local)} records")
 
 
+def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=4, seed=2024):
+    """replica_exchange_method (nem_order_mcmc.py:344-363) on net2: 10 replicas,
+    gamma_r = (1 + 0.2 r) S / E, `n_exchange` rounds of `n_iter` steps.  Each
+    round's replica_exchange_step result is recorded through a wrapper of the
+    module-level function (the reference itself runs unchanged)."""
+    adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
+    m = quiet(ref_nem.NEM, adj, end, err, s, e)
+    order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+    rounds = []
+    orig = ref_mcmc.replica_exchange_step
+
+    def recording_step(replicas, gammas, n_replicas, n_iters, scores, upwards):
+        out = orig(replicas, gammas, n_replicas, n_iters, scores, upwards)
+        best_score, best_nem, reps, sc, nex = out
+        rounds.append(dict(scores=np.array(sc, dtype=float), n_ex=nex, best=best_score,
+                           orders=np.array([np.asarray(r.perm_order) for r in reps]),
+                           best_orders=np.array([np.asarray(r.best_order) for r in reps])))
+        return out
+
+    random.seed(seed)
+    ref_mcmc.replica_exchange_step = recording_step
+    try:
+        best_score, best_nem = quiet(ref_mcmc.replica_exchange_method, m, n_exchange, n_iter, order)
+    finally:
+        ref_mcmc.replica_exchange_step = orig
+    np.savez_compressed(
+        os.path.join(HERE, "replica_net2.npz"), seed=seed, n_exchange=n_exchange, n_iter=n_iter,
+        order0=order, best_score=best_score, best_dag=np.asarray(best_nem.best_dag),
+        best_order=np.asarray(best_nem.best_order),
+        round_scores=np.array([r["scores"] for r in rounds]), round_nex=np.array([r["n_ex"] for r in rounds]),
+        round_best=np.array([r["best"] for r in rounds]), round_orders=np.array([r["orders"] for r in rounds]),
+        round_best_orders=np.array([r["best_orders"] for r in rounds]),
+        rng_state_after=np.array(random.getstate()[1], dtype=np.int64))
+    print("replica exchange:", best_score, [r["n_ex"] for r in rounds])
+
+
 def main():
     import scipy
     ref_nem, ref_mcmc, ref_utils = load_reference()
+    if "--only-replica" in sys.argv:
+        capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
+        return
     gen = repo_generator()
 
     # KAT from the reference's own test (tests/utils.tests.py:11-27): data only.
@@ -238,6 +277,8 @@ def main():
     mc2 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 16, 500)
     order2 = ref_utils.initial_order_guess(mc2.observed_knockdown_mat)
     capture_traj(ref_mcmc, mc2, order2, 2.0 * 16 / 500, 0.95, 20, "C2_20", record_local_every=7)
+
+    capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
 
     meta = dict(python=platform.python_version(), numpy=np.__version__, scipy=scipy.__version__,
                 machine=platform.machine(), processor=platform.processor(), reference=REF)

@@ -370,3 +370,34 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     eng.set_option("score_path", 1)
     assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-9
     eng.set_option("score_path", 0)
+
+
+def test_replica_exchange_net2_golden(net2):
+    """replica_exchange_method (nem_order_mcmc.py:344-363) on net2: 10
+    replicas, 3 rounds of 4 steps, global stream seeded 2024.  The batched
+    version (all replicas in one fused call per step) and the sequential
+    mirror both reproduce the reference's per-round scores, exchanges, final
+    best and random state."""
+    from nemo import nem_order_mcmc as mc
+    from nemo.replicas import ReplicaExchange
+    z = golden("replica_net2.npz")
+    m, _ = net2
+    order = utils.initial_order_guess(m.observed_knockdown_mat)
+    assert np.array_equal(order, z["order0"])
+    n_ex, n_it = int(z["n_exchange"]), int(z["n_iter"])
+    random.seed(int(z["seed"]))
+    rx = ReplicaExchange(m, order)
+    for k in range(n_ex):
+        best, best_obj, nx = rx.step(n_it, k % 2 == 0)
+        assert np.max(np.abs(rx.scores - z["round_scores"][k])) <= LL_TOL
+        assert nx == int(z["round_nex"][k])
+        assert abs(best - float(z["round_best"][k])) <= LL_TOL
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    win = rx.objs[best_obj]
+    assert np.array_equal(win.best_order, z["best_order"]) and np.array_equal(win.best_dag, z["best_dag"])
+    # the sequential mirror of the reference function
+    random.seed(int(z["seed"]))
+    best2, nem2 = mc.replica_exchange_method(m, n_ex, n_it, order)
+    assert abs(best2 - float(z["best_score"])) <= LL_TOL
+    assert np.array_equal(nem2.best_order, z["best_order"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
