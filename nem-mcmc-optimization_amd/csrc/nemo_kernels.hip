@@ -420,9 +420,16 @@ __device__ __forceinline__ int32_t pack_info(const LbfgsResult& r) {
   return (int32_t)(r.status | (nit << 4) | (nfev << 16));
 }
 
+// occupancy target of the local-optimum kernel: 3 waves per SIMD (168
+// VGPRs) hide more of the serial line-search latency than 2
+#ifndef NEMO_LOCAL_OPT_WAVES
+#define NEMO_LOCAL_OPT_WAVES 3
+#endif
+constexpr int kLocalOptWavesPerSimd = NEMO_LOCAL_OPT_WAVES;
+
 // pairs of the fused per-step scorer.  grid covers nchains * npairs waves.
 template <typename TT, int NPL>
-__global__ __launch_bounds__(256) void local_opt_pairs_kernel(
+__global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_kernel(
     int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
     const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
     const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
