@@ -15,7 +15,10 @@ import os
 import numpy as np
 
 _LIB = None
-_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libnemo.so")
+# NEMO_LIBRARY: load another build of the same C-ABI (tools/ablate.sh's
+# instrumented variants); the product path is the in-tree libnemo.so
+_PATH = os.environ.get("NEMO_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                       "libnemo.so")
 
 NEMO_F64, NEMO_F32 = 0, 1
 NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT = 0, -1, -2, -3, -5

@@ -44,12 +44,15 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
+    """Build the library (``out``/``defines``: instrumented variants for
+    tools/ablate.sh; the product is the default in-tree ``libnemo.so``)."""
+    target = out or LIB
+    if not force and out is None and up_to_date():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", SRC_DIR,
-           "-o", LIB + ".tmp"] + _sources()
+           *[f"-D{d}" for d in defines], "-o", target + ".tmp"] + _sources()
     if verbose:
         print(" ".join(cmd), flush=True)
     proc = subprocess.run(cmd, capture_output=True, text=True)
@@ -57,8 +60,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
     if verbose and proc.stderr.strip():
         print(proc.stderr, file=sys.stderr)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":

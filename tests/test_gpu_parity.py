@@ -367,6 +367,12 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
+    # 4 and 8 waves per block (auto switches at 384) give the same bits
+    for fk in (4, 6):
+        eng.set_option("fact_kernel", fk)
+        assert np.array_equal(eng.score(pos, w01), big)
+        assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
+    eng.set_option("fact_kernel", 0)
     eng.set_option("score_path", 1)
     assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-9
     eng.set_option("score_path", 0)
