@@ -29,6 +29,10 @@
 #ifndef NEMO_I8_ABLATE
 #define NEMO_I8_ABLATE 0
 #endif
+// register budget: waves per SIMD the int8 score kernel is compiled for
+#ifndef NEMO_I8_WAVES_PER_SIMD
+#define NEMO_I8_WAVES_PER_SIMD 2
+#endif
 
 namespace nemo {
 
@@ -185,18 +189,15 @@ __device__ __forceinline__ int i8_npass(int S, int cap) {
   return (cap == 0 || cap >= S - 1) ? (S + 1) / 2 : S;
 }
 
-// One 16-effect tile: NP pairs of i8 MFMAs per row block, the exact integer
-// recombination, f64 cells (U + G + T_0 2^(c-24) + T_1 2^(c-48)), and the
-// column log-sum-exp folded into (msum, lprod * 2^lexp).
+// One 16-effect tile, part 1: NP pairs of i8 MFMAs per row block and the
+// exact integer recombination into f64 cells (U + G + T_0 2^(c-24) +
+// T_1 2^(c-48)).  After this the U registers are free for the next tile.
 template <int NR, int NP>
-__device__ __forceinline__ void i8_tile(const i32x4* __restrict__ Al, const double* __restrict__ Gs,
-                                        const i32x4 b1, const double (&uc)[NR][4], double unull,
-                                        bool valid, int rg, double sA, double sB, double sC,
-                                        const double* __restrict__ etab, double& msum, double& lprod,
-                                        int& lexp) {
+__device__ __forceinline__ void i8_cells(const i32x4* __restrict__ Al, const double* __restrict__ Gs,
+                                         const i32x4 b1, const double (&uc)[NR][4], int rg, double sA,
+                                         double sB, double sC, double (&cell)[NR][4]) {
   constexpr int SPAD = NR * 16;
   const i32x4 b64 = b1 << 6;  // bytes 0/1 -> 0/64
-  double cell[NR][4];
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
     i32x4 acc[NP];
@@ -222,24 +223,41 @@ __device__ __forceinline__ void i8_tile(const i32x4* __restrict__ Al, const doub
       cell[r][g] = v + uc[r][g];
     }
   }
-  double m = unull;
+}
+
+// part 2: the column log-sum-exp over the SPAD rows and the null row, folded
+// into (msum, lprod * 2^lexp).  Max and sum run as pairwise trees (depth
+// log2(4 NR) instead of 4 NR: the tile is latency-bound at 2 waves/SIMD).
+template <int NR>
+__device__ __forceinline__ void i8_lse(double (&cell)[NR][4], double unull, bool valid,
+                                       const double* __restrict__ etab, double& msum,
+                                       double& lprod, int& lexp) {
+  constexpr int NC = 4 * NR;
+  double* c = &cell[0][0];
+  double mx[NC];
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
+  for (int k = 0; k < NC; ++k) mx[k] = c[k];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) m = vmax8(m, cell[r][g]);
+  for (int h = NC / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int k = 0; k < h; ++k) mx[k] = vmax8(mx[k], mx[k + h]);
+  double m = vmax8(mx[0], unull);
   m = vmax8(m, __shfl_xor(m, 16, kWave));
   m = vmax8(m, __shfl_xor(m, 32, kWave));
-  double l = 0.0;
+  double ex[NC];
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
+  for (int k = 0; k < NC; ++k) {
 #if NEMO_I8_ABLATE & 1  // instrumented build (tools/ablate.sh): no exp
-      l += cell[r][g] - m;
+    ex[k] = c[k] - m;
 #else
-      l += exp_lse8(cell[r][g] - m, etab);
+    ex[k] = exp_lse8(c[k] - m, etab);
 #endif
-    }
+  }
+#pragma unroll
+  for (int h = NC / 2; h >= 1; h /= 2)
+#pragma unroll
+    for (int k = 0; k < h; ++k) ex[k] += ex[k + h];
+  double l = ex[0];
   l += __shfl_xor(l, 16, kWave);
   l += __shfl_xor(l, 32, kWave);
   l += exp_lse8(unull - m, etab);
@@ -279,7 +297,7 @@ __device__ __forceinline__ void i8_tables(double* etab, double2* ltab, double* e
 // 1.5x slower at one block per CU and was dropped.)
 // ---------------------------------------------------------------------------
 template <int NR, int WAVES, int NP>
-__global__ __launch_bounds__(WAVES * kWave, 2) void score_i8_kernel(
+__global__ __launch_bounds__(WAVES * kWave, NEMO_I8_WAVES_PER_SIMD) void score_i8_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, int cexp,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
     const double* __restrict__ e_lo, const double* __restrict__ e_hi,
@@ -351,12 +369,8 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_i8_kernel(
       // (2NP * NR * 16 B per lane) in LDS instead of hoisted into registers
       uint32_t ao = a_lane;
       asm volatile("" : "+v"(ao));
-      const i32x4 b1 = bc;
-      double uu[NR][4];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) uu[r][g] = uc[r][g];
+      double cell[NR][4];
+      i8_cells<NR, NP>(ev.A + ao, ev.G, bc, uc, rg, sA, sB, sC, cell);
       const double unull = unc;
       int tn = t + 1, setn = set;
       if (tn >= min(ntiles, 8 * set + 8)) {
@@ -364,9 +378,8 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_i8_kernel(
         tn = 8 * setn;
       }
       const bool more = setn < s_end;
-      if (more) load_tile(tn);
-      i8_tile<NR, NP>(ev.A + ao, ev.G, b1, uu, unull, t * 16 + col < E, rg, sA, sB, sC, etab, msum,
-                      lprod, lexp);
+      if (more) load_tile(tn);  // into the registers the cells just freed
+      i8_lse<NR>(cell, unull, t * 16 + col < E, etab, msum, lprod, lexp);
       if (setn != set) {  // set complete: one partial
         const double v = i8_set_value(msum, lprod, lexp, lane);
         if (lane == 0) partial[(size_t)b * nsets + set] = v;
