@@ -2,6 +2,7 @@
 golden vectors and the pinned oracle.  Tolerances (north_star): log-scores
 within 1e-6 absolute in fp64; the fp32 table path (C5) within 1e-6 relative;
 accepted-move indices of the sampler identical under the reference's seed."""
+import os
 import random
 
 import numpy as np
@@ -407,3 +408,28 @@ def test_replica_exchange_net2_golden(net2):
     assert abs(best2 - float(z["best_score"])) <= LL_TOL
     assert np.array_equal(nem2.best_order, z["best_order"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_integration_stub_binds_the_library(net2):
+    """INTEGRATION.md's ctypes stub (the binding a maintainer would add next to
+    the reference) drives libnemo.so for a sampler object with the reference's
+    attributes and gives the mirror's results."""
+    import re
+
+    from nemo import _lib
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    text = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "INTEGRATION.md")).read()
+    code = re.search(r"```python\n(# nemo_binding\.py.*?)```", text, re.S).group(1)
+    code = code.replace('"/path/to/nem-mcmc-optimization_amd/nemo/libnemo.so"', repr(_lib.lib_path()))
+    ns = {}
+    exec(compile(code, "nemo_binding.py", "exec"), ns)
+    m, _ = net2
+    order = utils.initial_order_guess(m.observed_knockdown_mat)
+    ref = NEMOrderMCMC(m, order)
+    smp = NEMOrderMCMC(m, order, engine=ref.engine)
+    scorer = ns["Scorer"](smp)
+    want = ref.get_optimal_weights(init=True)
+    got = scorer.optimal_weights(smp)
+    assert got == want and np.array_equal(smp.parent_weights, ref.parent_weights)  # same kernels, same bits
+    _ow, ll = scorer.order_score(smp)
+    assert abs(ll - float(ref.engine.score(ref._pos[None], expit(ref.parent_weights)[None])[0])) <= 1e-9
