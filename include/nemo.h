@@ -73,6 +73,15 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains);
 
 /* ---- A1/A2: stage the model once (nem.py:25-64 outputs) ---------------- */
 int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T);
+/* the same model built on the device from the observed knockdown matrix
+ * (nem.py:25-64, the tables NEM.__init__ derives, nem_order_mcmc.py:44):
+ *   D [S][E] bytes in {0,1} (NEM.observed_knockdown_mat), A = log(alpha/(1-beta)),
+ *   B = log(beta/(1-alpha)) (NEM.A, NEM.B, nem.py:17-18).
+ * T[i][j] = where(D[j]==0, B, -A) off the diagonal, T[i][i] = U[i] with
+ * U[i] = where(D[i]==1, 0, B) + A per other 1 in the column, U[S] = A per 1.
+ * Stages bit-for-bit what nemo_stage_tables stages for those U and T, with
+ * no S*S*E host table (655 MB at C5 in fp64). */
+int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B);
 
 /* ---- A4+A5: batched order-score evaluation --------------------------------
  * Replaces NEMOrderMCMC.compute_cell_ratios + calculate_ll

@@ -174,99 +174,47 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
   return NEMO_OK;
 }
 
-int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
-  int rc = check_ctx(ctx, false);
-  if (rc) return rc;
-  if (!U || !T) return fail(NEMO_ERR_ARG, "null table");
-  Ctx& c = ctx->c;
-  const size_t S = c.S, E = c.E, n = S * S * E;
-  // range of the off-diagonal rows (the ones the score reads)
-  double amax = 0.0;
-  for (size_t i = 0; i < S; ++i)
-    for (size_t j = 0; j < S; ++j) {
-      if (i == j) continue;
-      const double* r = T + (i * S + j) * E;
-      for (size_t e = 0; e < E; ++e) {
-        const double v = r[e];
-        if (!isfinite(v)) return fail(NEMO_ERR_ARG, "T[%zu][%zu][%zu] is not finite", i, j, e);
-        amax = std::max(amax, fabs(v));
-      }
-    }
-  const double lim = c.dtype == NEMO_F64 ? 170.0 : 20.0;
-  if (amax > lim)
-    return fail(NEMO_ERR_ARG, "|T| up to %g exceeds the %s product range (%g)", amax,
-                c.dtype == NEMO_F64 ? "f64" : "f32", lim);
-  for (size_t k = 0; k < (S + 1) * E; ++k)
-    if (isnan(U[k])) return fail(NEMO_ERR_ARG, "U has NaN");
-  HIPCHK(hipStreamSynchronize(c.stream));
-  const size_t esz = c.dtype == NEMO_F64 ? 8 : 4;
-  if (c.d_eT) hipFree(c.d_eT);
-  if (c.d_U) hipFree(c.d_U);
-  c.d_eT = c.d_U = nullptr;
-  HIPCHK(hipMalloc(&c.d_eT, n * esz));
-  HIPCHK(hipMalloc(&c.d_U, (S + 1) * E * esz));
-  double* d_t64 = nullptr;
-  HIPCHK(hipMalloc((void**)&d_t64, n * sizeof(double)));
-  HIPCHK(hipMemcpyAsync(d_t64, T, n * sizeof(double), hipMemcpyHostToDevice, c.stream));
-  HIPCHK(nemo::launch_exp_table(c, d_t64, c.stream));
-  if (c.dtype == NEMO_F64) {
-    HIPCHK(hipMemcpyAsync(c.d_U, U, (S + 1) * E * 8, hipMemcpyHostToDevice, c.stream));
-  } else {
-    std::vector<float> u32((S + 1) * E);
-    for (size_t k = 0; k < u32.size(); ++k) u32[k] = (float)U[k];
-    HIPCHK(hipMemcpyAsync(c.d_U, u32.data(), u32.size() * 4, hipMemcpyHostToDevice, c.stream));
-    HIPCHK(hipStreamSynchronize(c.stream));
-  }
-  HIPCHK(hipStreamSynchronize(c.stream));
-  HIPCHK(hipFree(d_t64));
-  c.table_absmax = amax;
+}  // extern "C"
 
-  // factored form: every off-diagonal row j identical for all children and
-  // two-valued (nem.py:44-46 builds exactly that)
-  const int nwords = (int)((E + 63) / 64);
-  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
-  std::vector<double> elo(S), ehi(S);
-  bool fact = true;
-  for (size_t j = 0; j < S && fact; ++j) {
-    const size_t i0 = (j == 0) ? 1 : 0;
-    const double* L = T + (i0 * S + j) * E;
-    for (size_t i = 0; i < S && fact; ++i)
-      if (i != j && i != i0 && memcmp(T + (i * S + j) * E, L, E * sizeof(double)) != 0) fact = false;
-    const double lo = L[0];
-    double hi = lo;
-    bool have_hi = false;
-    for (size_t e = 0; e < E && fact; ++e) {
-      const double v = L[e];
-      if (v == lo) continue;
-      if (!have_hi) { hi = v; have_hi = true; }
-      if (v != hi) { fact = false; break; }
-      d1[j * nwords + e / 64] |= 1ull << (e % 64);
+namespace {
+
+// (re)allocate the table buffers of a staging: exp(T) and U in the table
+// dtype, U in fp64 padded to the factored row blocking (the int8 kernel reads
+// padding rows unclamped, their G hides them) plus one zeroed 16-effect tile
+// (the factored kernels read whole tiles; lanes past E are masked out)
+int alloc_tables(Ctx& c) {
+  const size_t S = c.S, E = c.E;
+  const size_t esz = c.dtype == NEMO_F64 ? 8 : 4;
+  HIPCHK(hipStreamSynchronize(c.stream));
+  c.staged = false;
+  void** bufs[] = {&c.d_eT, &c.d_U, (void**)&c.d_U64};
+  for (void** p : bufs)
+    if (*p) {
+      hipFree(*p);
+      *p = nullptr;
     }
-    elo[j] = exp(lo);
-    ehi[j] = exp(hi);
-  }
-  // the factored kernels' exp takes finite arguments: U must be finite too
-  for (size_t k = 0; k < (S + 1) * E && fact; ++k)
-    if (!isfinite(U[k]) || fabs(U[k]) > 1e9) fact = false;
-  c.factored = fact;
-  c.fspad = nemo::factored_spad(c.S);
-  c.nwords = nwords;
-  if (c.d_U64) hipFree(c.d_U64);
-  c.d_U64 = nullptr;
-  // rows up to the factored row padding (zero; the int8 kernel reads padding
-  // rows unclamped, their G hides them) + one zeroed 16-effect tile (the
-  // factored kernels read whole tiles; lanes past E are masked out)
+  HIPCHK(hipMalloc(&c.d_eT, S * S * E * esz));
+  HIPCHK(hipMalloc(&c.d_U, (S + 1) * E * esz));
   const size_t urows = std::max(S + 1, (size_t)std::max(nemo::factored_spad(c.S), 0));
   HIPCHK(hipMalloc((void**)&c.d_U64, (urows * E + 16) * 8));
   HIPCHK(hipMemset(c.d_U64, 0, (urows * E + 16) * 8));
-  HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
+  return NEMO_OK;
+}
+
+// the factored form once T's structure is known: every off-diagonal row j is
+// shared by all children and takes lo_j or hi_j (bit d1[j][e] = 1: hi_j)
+int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
+                   const std::vector<double>& elo, const std::vector<double>& ehi) {
+  Ctx& c = ctx->c;
+  const size_t S = c.S, E = c.E;
+  const int nwords = (int)((E + 63) / 64);
+  c.factored = fact;
+  c.fspad = nemo::factored_spad(c.S);
+  c.nwords = nwords;
   if (fact) {
-    if (c.d_D1w) hipFree(c.d_D1w);
-    if (c.d_elo) hipFree(c.d_elo);
-    if (c.d_ehi) hipFree(c.d_ehi);
-    HIPCHK(hipMalloc((void**)&c.d_D1w, d1.size() * 8));
-    HIPCHK(hipMalloc((void**)&c.d_elo, S * 8));
-    HIPCHK(hipMalloc((void**)&c.d_ehi, S * 8));
+    HIPCHK(dalloc(&c.d_D1w, d1.size()));
+    HIPCHK(dalloc(&c.d_elo, S));
+    HIPCHK(dalloc(&c.d_ehi, S));
     HIPCHK(hipMemcpy(c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
@@ -305,6 +253,156 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
   }
   c.staged = true;
   return NEMO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!U || !T) return fail(NEMO_ERR_ARG, "null table");
+  Ctx& c = ctx->c;
+  const size_t S = c.S, E = c.E, n = S * S * E;
+  // range of the off-diagonal rows (the ones the score reads)
+  double amax = 0.0;
+  for (size_t i = 0; i < S; ++i)
+    for (size_t j = 0; j < S; ++j) {
+      if (i == j) continue;
+      const double* r = T + (i * S + j) * E;
+      for (size_t e = 0; e < E; ++e) {
+        const double v = r[e];
+        if (!isfinite(v)) return fail(NEMO_ERR_ARG, "T[%zu][%zu][%zu] is not finite", i, j, e);
+        amax = std::max(amax, fabs(v));
+      }
+    }
+  const double lim = c.dtype == NEMO_F64 ? 170.0 : 20.0;
+  if (amax > lim)
+    return fail(NEMO_ERR_ARG, "|T| up to %g exceeds the %s product range (%g)", amax,
+                c.dtype == NEMO_F64 ? "f64" : "f32", lim);
+  for (size_t k = 0; k < (S + 1) * E; ++k)
+    if (isnan(U[k])) return fail(NEMO_ERR_ARG, "U has NaN");
+  if ((rc = alloc_tables(c))) return rc;
+  double* d_t64 = nullptr;
+  HIPCHK(hipMalloc((void**)&d_t64, n * sizeof(double)));
+  HIPCHK(hipMemcpyAsync(d_t64, T, n * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  HIPCHK(nemo::launch_exp_table(c, d_t64, c.stream));
+  if (c.dtype == NEMO_F64) {
+    HIPCHK(hipMemcpyAsync(c.d_U, U, (S + 1) * E * 8, hipMemcpyHostToDevice, c.stream));
+  } else {
+    std::vector<float> u32((S + 1) * E);
+    for (size_t k = 0; k < u32.size(); ++k) u32[k] = (float)U[k];
+    HIPCHK(hipMemcpyAsync(c.d_U, u32.data(), u32.size() * 4, hipMemcpyHostToDevice, c.stream));
+    HIPCHK(hipStreamSynchronize(c.stream));
+  }
+  HIPCHK(hipStreamSynchronize(c.stream));
+  HIPCHK(hipFree(d_t64));
+  HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
+  c.table_absmax = amax;
+
+  // factored form: every off-diagonal row T[.][j] identical for all children
+  // and two-valued (nem.py:44-46 builds exactly that); lo_j = its first value
+  const int nwords = (int)((E + 63) / 64);
+  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
+  std::vector<double> elo(S), ehi(S);
+  bool fact = true;
+  for (size_t j = 0; j < S && fact; ++j) {
+    const size_t i0 = (j == 0) ? 1 : 0;
+    const double* L = T + (i0 * S + j) * E;
+    for (size_t i = 0; i < S && fact; ++i)
+      if (i != j && i != i0 && memcmp(T + (i * S + j) * E, L, E * sizeof(double)) != 0) fact = false;
+    const double lo = L[0];
+    double hi = lo;
+    bool have_hi = false;
+    for (size_t e = 0; e < E && fact; ++e) {
+      const double v = L[e];
+      if (v == lo) continue;
+      if (!have_hi) { hi = v; have_hi = true; }
+      if (v != hi) { fact = false; break; }
+      d1[j * nwords + e / 64] |= 1ull << (e % 64);
+    }
+    elo[j] = exp(lo);
+    ehi[j] = exp(hi);
+  }
+  // the factored kernels' exp takes finite arguments: U must be finite too
+  for (size_t k = 0; k < (S + 1) * E && fact; ++k)
+    if (!isfinite(U[k]) || fabs(U[k]) > 1e9) fact = false;
+  return stage_factored(ctx, fact, d1, elo, ehi);
+}
+
+int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!D) return fail(NEMO_ERR_ARG, "null knockdown matrix");
+  Ctx& c = ctx->c;
+  const size_t S = c.S, E = c.E;
+  if (!isfinite(A) || !isfinite(B)) return fail(NEMO_ERR_ARG, "A=%g B=%g must be finite", A, B);
+  // the values present in the off-diagonal rows (S >= 2: every row j is one)
+  bool has0 = false, has1 = false;
+  std::vector<int> colsum(E, 0);
+  for (size_t j = 0; j < S; ++j)
+    for (size_t e = 0; e < E; ++e) {
+      const uint8_t d = D[j * E + e];
+      if (d > 1) return fail(NEMO_ERR_ARG, "D[%zu][%zu] = %d is not 0 or 1", j, e, (int)d);
+      has0 |= d == 0;
+      has1 |= d == 1;
+      colsum[e] += d;
+    }
+  const double amax = std::max(has0 ? fabs(B) : 0.0, has1 ? fabs(A) : 0.0);
+  const double lim = c.dtype == NEMO_F64 ? 170.0 : 20.0;
+  if (amax > lim)
+    return fail(NEMO_ERR_ARG, "|T| up to %g exceeds the %s product range (%g)", amax,
+                c.dtype == NEMO_F64 ? "f64" : "f32", lim);
+  // the addition chains of compute_scores (nem.py:25-34), in its order
+  std::vector<double> chains(2 * (S + 1));
+  chains[0] = 0.0;
+  chains[S + 1] = B;
+  for (size_t k = 1; k <= S; ++k) {
+    chains[k] = chains[k - 1] + A;
+    chains[S + 1 + k] = chains[S + k] + A;
+  }
+  // U's entries are chain elements: the ones indexed must be finite (NaN
+  // cannot arise from finite A, B) and, for the factored kernels, <= 1e9
+  bool ufin = true;
+  for (size_t e = 0; e < E; ++e) {
+    const int k = colsum[e];
+    const double vs[3] = {chains[k], k > 0 ? chains[k - 1] : 0.0, chains[S + 1 + k]};
+    for (double v : vs) ufin &= isfinite(v) && fabs(v) <= 1e9;
+  }
+  if ((rc = alloc_tables(c))) return rc;
+  uint8_t* d_D = nullptr;
+  double* d_chains = nullptr;
+  HIPCHK(hipMalloc((void**)&d_D, S * E));
+  HIPCHK(hipMalloc((void**)&d_chains, chains.size() * 8));
+  HIPCHK(hipMemcpyAsync(d_D, D, S * E, hipMemcpyHostToDevice, c.stream));
+  HIPCHK(hipMemcpyAsync(d_chains, chains.data(), chains.size() * 8, hipMemcpyHostToDevice, c.stream));
+  HIPCHK(nemo::launch_knockdown_tables(c, d_D, d_chains, A, B, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  HIPCHK(hipFree(d_D));
+  HIPCHK(hipFree(d_chains));
+  c.table_absmax = amax;
+
+  // factored form straight from D, with nemo_stage_tables' conventions:
+  // lo_j = row j's first value, bit = "not lo_j"
+  const int nwords = (int)((E + 63) / 64);
+  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
+  std::vector<double> elo(S), ehi(S);
+  const double negA = -A;
+  for (size_t j = 0; j < S; ++j) {
+    const uint8_t* r = D + j * E;
+    const double lo = r[0] ? negA : B;
+    double hi = lo;
+    for (size_t e = 0; e < E; ++e) {
+      const double v = r[e] ? negA : B;
+      if (v == lo) continue;
+      hi = v;
+      d1[j * nwords + e / 64] |= 1ull << (e % 64);
+    }
+    elo[j] = exp(lo);
+    ehi[j] = exp(hi);
+  }
+  return stage_factored(ctx, ufin, d1, elo, ehi);
 }
 
 static bool use_factored(const Ctx& c) {

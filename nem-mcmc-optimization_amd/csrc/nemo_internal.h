@@ -89,6 +89,11 @@ struct Ctx {
 // ---- launchers (nemo_kernels.hip); all enqueue on `st` and never allocate ----
 // exp() of the staged table (in place conversion from fp64 host layout)
 hipError_t launch_exp_table(Ctx& c, const double* d_T64, hipStream_t st);
+// staging from the knockdown matrix (nemo_stage.hip): d_D [S][E] bytes in
+// {0,1}, d_chains [2][S+1] = (0 + k A, B + k A); writes d_U64 (S+1 rows), d_U
+// and d_eT
+hipError_t launch_knockdown_tables(Ctx& c, const uint8_t* d_D, const double* d_chains, double A,
+                                   double B, hipStream_t st);
 hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                        int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
                        hipStream_t st);

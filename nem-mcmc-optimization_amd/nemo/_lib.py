@@ -25,6 +25,7 @@ NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT = 0, -1, -2, -
 
 _i32p = C.POINTER(C.c_int32)
 _f64p = C.POINTER(C.c_double)
+_u8p = C.POINTER(C.c_uint8)
 _vp = C.c_void_p
 
 # (name, restype, argtypes) -- one line per symbol of include/nemo.h
@@ -36,6 +37,7 @@ SIGNATURES = [
     ("nemo_ctx_destroy", None, [_vp]),
     ("nemo_reserve", C.c_int, [_vp, C.c_int, C.c_int]),
     ("nemo_stage_tables", C.c_int, [_vp, _f64p, _f64p]),
+    ("nemo_stage_knockdown", C.c_int, [_vp, _u8p, C.c_double, C.c_double]),
     ("nemo_score", C.c_int, [_vp, C.c_int, _i32p, _f64p, C.c_int, _f64p, _f64p, _f64p, _f64p]),
     ("nemo_score_dev", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("nemo_score_group_dev", C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int, _vp, _vp]),

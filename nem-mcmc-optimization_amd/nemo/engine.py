@@ -28,7 +28,6 @@ class Engine:
     """
 
     def __init__(self, U, T, device: int = 0, dtype: str = "f64"):
-        lib = _lib.load()
         U = f64(U)
         T = f64(T)
         if T.ndim != 3 or T.shape[0] != T.shape[1]:
@@ -36,20 +35,45 @@ class Engine:
         S, _, E = T.shape
         if U.shape != (S + 1, E):
             raise ValueError(f"U must be ({S + 1}, {E}), got {U.shape}")
+        self._create(S, E, device, dtype)
+        check(_lib.load().nemo_stage_tables(self._ctx, ptr(U), ptr(T)))
+
+    def _create(self, S, E, device, dtype):
+        lib = _lib.load()
         self.S, self.E, self.device, self.dtype = S, E, device, dtype
         self._ctx = C.c_void_p()
         check(lib.nemo_ctx_create(device, S, E, _DTYPES[dtype], C.byref(self._ctx)))
         self._fin = weakref.finalize(self, lib.nemo_ctx_destroy, self._ctx)
-        check(lib.nemo_stage_tables(self._ctx, ptr(U), ptr(T)))
+
+    @classmethod
+    def from_knockdown(cls, D, A, B, device: int = 0, dtype: str = "f64") -> "Engine":
+        """The model built on the GPU from the observed knockdown matrix D
+        (S, E) with entries 0/1 and the NEM's A, B (nem.py:17-18, 25-64):
+        the same staged tables as ``Engine(U, T)`` with the reference's U and
+        T, without the S*S*E host table."""
+        D = np.asarray(D)
+        if D.ndim != 2:
+            raise ValueError(f"D must be (S, E), got {D.shape}")
+        if not np.isin(D, (0, 1)).all():
+            raise ValueError("D must hold only 0 and 1")
+        d8 = np.ascontiguousarray(D, dtype=np.uint8)
+        self = cls.__new__(cls)
+        self._create(d8.shape[0], d8.shape[1], device, dtype)
+        check(_lib.load().nemo_stage_knockdown(self._ctx, d8.ctypes.data_as(_lib._u8p),
+                                               float(A), float(B)))
+        return self
 
     # -- cached engines per model -----------------------------------------
     @classmethod
     def for_nem(cls, nem, device: int = 0, dtype: str = "f64") -> "Engine":
+        """The model's engine (one per device and dtype), staged from its
+        knockdown matrix on the GPU (``from_knockdown``)."""
         cache = nem.__dict__.setdefault("_nemo_engines", {})
         key = (device, dtype)
         eng = cache.get(key)
         if eng is None:
-            eng = cls(nem.U, nem.get_score_tensor(), device=device, dtype=dtype)
+            eng = cls.from_knockdown(nem.observed_knockdown_mat, nem.A, nem.B, device=device,
+                                     dtype=dtype)
             cache[key] = eng
         return eng
 

@@ -36,6 +36,39 @@ def _addition_chain(start: float, step: float, count: int) -> np.ndarray:
     return chain
 
 
+class ScoreTables:
+    """Lazy stand-in for the reference's list of S score tables (nem.py:49-54):
+    indexable, iterable, sized; T[i] is built on access."""
+
+    def __init__(self, nem, knockdown_mat):
+        self._nem = nem
+        self._d = knockdown_mat
+
+    def __len__(self):
+        return self._nem.num_s
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[k] for k in range(*i.indices(len(self)))]
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        return self._nem.build_score_table(i, self._d)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def __array__(self, dtype=None, copy=None):
+        t = self._nem.get_score_tensor(self._d)
+        return t if dtype is None else t.astype(dtype, copy=False)
+
+    @property
+    def knockdown_mat(self):
+        return self._d
+
+
 class NEM:
     """Reference: nem.py:8-22.
 
@@ -68,7 +101,9 @@ class NEM:
         self.observed_knockdown_mat = utils.create_observed_knockdown_mat(
             self.real_knockdown_mat, alpha, beta)
         self._tensor_cache = None
-        self.U = self.get_node_lr_table(self.get_score_tables(self.observed_knockdown_mat))
+        # U without the S*S*E table: the diagonal rows by their closed form
+        # (bit-identical to get_node_lr_table(get_score_tables(D)), tested)
+        self.U = self._node_lr_table_direct()
         # compute_real_score side effect (nem.py:90-91): diagonal of the
         # caller's adjacency zeroed in place.
         for i in range(self.num_s):
@@ -99,9 +134,13 @@ class NEM:
         return table
 
     def get_score_tables(self, knockdown_mat):
-        """List of S tables (S, E).  Reference: nem.py:49-54."""
-        tensor = self.get_score_tensor(knockdown_mat)
-        return [tensor[i] for i in range(self.num_s)]
+        """The S tables (S, E).  Reference: nem.py:49-54 (a list of arrays).
+
+        Returned as a lazy sequence: ``tables[i]`` builds T[i] on access and
+        ``np.asarray(tables)`` the whole tensor, so a sampler that only hands
+        the model to the GPU (which builds its tables from D itself,
+        ``nemo_stage_knockdown``) never holds the S*S*E table on the host."""
+        return ScoreTables(self, knockdown_mat)
 
     def get_score_tensor(self, knockdown_mat=None) -> np.ndarray:
         """The score tables as one C-contiguous (S, S, E) float64 tensor
@@ -122,6 +161,14 @@ class NEM:
         return tensor
 
     # -- A2: node LR table --------------------------------------------------
+    def _node_lr_table_direct(self):
+        d = np.asarray(self.observed_knockdown_mat)
+        chain0, chainb = self._chains()
+        k = ((d == 1).sum(axis=0)[None, :] - (d == 1)).astype(np.int64)
+        rows = np.where(d == 1, chain0[k], chainb[k])
+        null_row = chain0[(d != 0).sum(axis=0)]
+        return np.vstack([rows, null_row[None, :]])
+
     def get_node_lr_table(self, all_score_tables):
         """Rows 0..S-1: diagonal rows ``T[i][i]``; row S: sum over S-genes of
         where(D==0, 0, A), added row by row.  Reference: nem.py:56-64."""

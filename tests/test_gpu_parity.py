@@ -433,3 +433,55 @@ def test_integration_stub_binds_the_library(net2):
     assert got == want and np.array_equal(smp.parent_weights, ref.parent_weights)  # same kernels, same bits
     _ow, ll = scorer.order_score(smp)
     assert abs(ll - float(ref.engine.score(ref._pos[None], expit(ref.parent_weights)[None])[0])) <= 1e-9
+
+
+@pytest.mark.parametrize("s,e,dtype,cap", [(11, 184, "f64", 0), (16, 500, "f64", 0), (64, 2000, "f64", 0),
+                                           (128, 700, "f32", 6)])
+def test_stage_knockdown_equals_stage_tables(s, e, dtype, cap):
+    """Staging from D on the device (nemo_stage_knockdown, nem.py:25-64)
+    stages bit for bit what the host tables stage: the same cells and ll on
+    every kernel, the same fused optimal-weights step, and U itself (cells of
+    an evaluation with all weights 0)."""
+    m = generator.synthetic_nem(s, e, 3)
+    ref = Engine(m.U, m.get_score_tensor(), dtype=dtype)
+    dev = Engine.from_knockdown(m.observed_knockdown_mat, m.A, m.B, dtype=dtype)
+    assert dev.factored == ref.factored
+    rng = np.random.default_rng(s + e)
+    pos = np.array([rng.permutation(s) for _ in range(6)], dtype=np.int32)
+    w01 = expit(rng.uniform(-3, 3, (6, s, s)))
+    zero = dev.score(pos[:1], np.zeros((1, s, s)), cap=cap, want_cells=True)["cells"][0]
+    assert np.array_equal(zero, ref.score(pos[:1], np.zeros((1, s, s)), cap=cap, want_cells=True)["cells"][0])
+    if dtype == "f64":
+        assert np.array_equal(zero, m.U)
+    for path, fks in ((1, (0,)), (2, (0, 1, 2, 4, 6) if s <= 64 else (0, 1))):
+        for fk in fks:
+            for eng in (ref, dev):
+                eng.set_option("score_path", path)
+                eng.set_option("fact_kernel", fk)
+            a = ref.score(pos, w01, cap=cap, want_cells=True)
+            b = dev.score(pos, w01, cap=cap, want_cells=True)
+            assert np.array_equal(a["ll"], b["ll"]), (path, fk)
+            assert np.array_equal(a["cells"], b["cells"]), (path, fk)
+            assert np.array_equal(ref.score(pos, w01, cap=cap), dev.score(pos, w01, cap=cap)), (path, fk)
+    for eng in (ref, dev):
+        eng.set_option("score_path", 0)
+        eng.set_option("fact_kernel", 0)
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    wr = rng.uniform(-3, 3, (2, s, s))
+    anc = np.clip(rng.random((2, s, s)) - 0.5, 0, 1)
+    ra = ref.optimal_weights(pos[:2], expit(wr), anc, wr, SIG0, SIG1, cap=cap, raise_on_fail=False)
+    rb = dev.optimal_weights(pos[:2], expit(wr), anc, wr, SIG0, SIG1, cap=cap, raise_on_fail=False)
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x, y)
+    ref.close()
+    dev.close()
+
+
+def test_stage_knockdown_rejects_bad_input():
+    m = generator.synthetic_nem(4, 10, 0)
+    with pytest.raises(ValueError, match="0 and 1"):
+        Engine.from_knockdown(m.observed_knockdown_mat * 0.5, m.A, m.B)
+    with pytest.raises(RuntimeError, match="finite"):
+        Engine.from_knockdown(m.observed_knockdown_mat, float("-inf"), m.B)
+    with pytest.raises(RuntimeError, match="product range"):
+        Engine.from_knockdown(m.observed_knockdown_mat, m.A, 30.0, dtype="f32")

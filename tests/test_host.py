@@ -26,6 +26,23 @@ def test_net2_model_bit_exact(net2):
     assert np.array_equal(m.adj_matrix, z["adj_after"])
 
 
+def test_lazy_tables_and_direct_u():
+    """The constructor's U (closed form, no S*S*E table) equals the
+    reference's get_node_lr_table(get_score_tables(D)) bit for bit, and the
+    lazy table sequence behaves like the reference's list."""
+    for s, e, seed in ((11, 184, 0), (16, 500, 0), (40, 300, 7)):
+        m = generator.synthetic_nem(s, e, seed)
+        tables = m.get_score_tables(m.observed_knockdown_mat)
+        t = m.get_score_tensor()
+        assert len(tables) == s
+        assert np.array_equal(m.U, m.get_node_lr_table([t[i] for i in range(s)]))
+        assert np.array_equal(np.asarray(tables), t)
+        assert np.array_equal(tables[-1], t[s - 1]) and np.array_equal(tables[3][1], t[3][1])
+        assert all(np.array_equal(a, b) for a, b in zip(tables, t))
+        with pytest.raises(IndexError):
+            tables[s]
+
+
 def test_initial_order_guess(net2):
     m, _ = net2
     assert np.array_equal(utils.initial_order_guess(m.observed_knockdown_mat), golden("net2_tables.npz")["order0"])
