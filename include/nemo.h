@@ -136,6 +136,32 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
 
+/* ---- fixed-order optimizers of methods.py ---------
+ * Every call handles nprob independent problems (one order each) with host
+ * buffers; w / w_out are [nprob][S][S] (w_out = w with every permissible pair
+ * replaced by its optimum), ll_out [nprob] is the sweep's evaluation, info
+ * (nullable) as for nemo_optimal_weights.  NEMO_ERR_OPT (results written)
+ * when a local optimisation fails, where the reference raises
+ * (methods.py:115, :394).
+ *
+ * Method.opt_gamma (methods.py:397-405): evaluation on the raw weights in
+ * [0, 1], then per pair minimize(local_ll_sum_gamma (:8-9), x0 = w[i][k],
+ * bounds [(0, 1)], jac=True, tol=0.01) with c from exp(T[i][k]) and order
+ * weights row k (:385-395).  cap as for nemo_score (0 = the reference). */
+int nemo_gamma_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, int cap,
+                     double* w_out, double* ll_out, int32_t* info);
+/* InverseMethod (methods.py:21-172): w holds log-weights (-5000 off the
+ * parents).  out = unorder_arr(order, B / (1 + B)) with B =
+ * solve_triangular(I - order_arr(order, exp(w)), I, lower=True)
+ * (:118-121, :160-164). */
+int nemo_inverse_ancestral(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, double* out);
+/* InverseMethod.opt_b (:117-129): evaluation on B/(1+B), then every pair
+ * in the reference's loop order minimises local_ll_sum_b_inv (:73-82),
+ * bounds [(-5000, 500)], eps 1e-3, tol 0.1, each pair seeing the optima of
+ * the pairs before it (levels of independent pairs on the device). */
+int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, double* w_out,
+                       double* ll_out, int32_t* info);
+
 /* ---- options -------------------------------------------------------------
  *   "xcd_remap"  1 (default) XCD-aware block order; speed only
  *   "score_path" 0 (default) auto: the factored MFMA kernel when the staged

@@ -132,6 +132,7 @@ struct Dcsrch {
   int stage;
   double finit, ginit, gtest, width, width1;
   double stx, fx, gx, sty, fy, gy, stmin, stmax;
+  double stpmax = kStpMax;  // lnsrlb's stpmx (1e10 unbounded; from the bounds otherwise)
 
   // returns false on ERROR (initial derivative not negative)
   __device__ __forceinline__ bool start(double stp, double f, double g) {
@@ -142,7 +143,7 @@ struct Dcsrch {
     finit = f;
     ginit = g;
     gtest = kFtolLs * g;
-    width = kStpMax - 0.0;
+    width = stpmax - 0.0;
     width1 = width / 0.5;
     stx = 0.0; fx = f; gx = g;
     sty = 0.0; fy = f; gy = g;
@@ -155,7 +156,7 @@ struct Dcsrch {
   // 1 = CONV, 2 = WARN
   __device__ __forceinline__ int step(double& stp, double f, double g) {
 #pragma clang fp contract(off)
-    const double stpmin = 0.0, stpmax = kStpMax;
+    const double stpmin = 0.0;
     const double ftest = finit + stp * gtest;
     if (stage == 1 && f <= ftest && g >= 0.0) stage = 2;
     int task = 0;
@@ -207,22 +208,49 @@ struct Dcsrch {
   }
 };
 
+// projgr: the projected gradient of one variable
+template <bool BOUNDED>
+__device__ __forceinline__ double projg(double x, double g, bool has_lo, double lo, bool has_hi, double hi) {
+  if (!BOUNDED) return g;
+  if (g < 0.0) return has_hi ? dmax(x - hi, g) : g;
+  return has_lo ? dmin(x - lo, g) : g;
+}
+
 }  // namespace lb
 
-// Minimise a 1-D objective from x0.  `fg(x, x1, f0, f1)` must return the
-// objective at x and at x1 (identical in all lanes).  Written as a state
-// machine with ONE evaluation site so the (large, fully unrolled) objective
-// body is instantiated once.
-template <class FG>
-__device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, double ftol = 0.01, double gtol = 0.01,
-                                        double eps = 1e-8, int maxls = 20, int maxiter = 15000,
-                                        int maxfun = 15000) {
+// Options of the bounded / analytic-gradient variant (the fixed-order
+// optimizers of methods.py: bounds [(0, 1)] with jac=True at :393,
+// [(-5000, 500)] with eps=1e-3 and tol=0.1 at :110).
+struct LbOpts {
+  double ftol = 0.01, gtol = 0.01, eps = 1e-8;
+  double lo = -__builtin_inf(), hi = __builtin_inf();
+  int maxls = 20, maxiter = 15000, maxfun = 15000;
+};
+
+// Minimise a 1-D objective from x0.  Without gradient (ANALYTIC = false)
+// `fg(x, x1, f0, f1)` must return the objective at x and at x1; with it,
+// `fg(x, f, g)` returns the objective and its derivative at x (identical in
+// all lanes).  BOUNDED runs L-BFGS-B 3.0's constrained branch (cnstnd, and
+// boxed when both bounds are finite, as in every bounded call the reference
+// makes): x0 clipped, projected gradient, the generalised Cauchy point stops
+// at the bound when the model minimiser lies beyond it, unit first trial
+// step, stpmax from the bounds, forward differences flipped inside the box
+// (scipy _numdiff._adjust_scheme_to_bounds).  Written as a state machine
+// with ONE evaluation site so the (large, fully unrolled) objective body is
+// instantiated once.  Python specification: oracle/lbfgsb1.py minimize_1d.
+template <bool BOUNDED, bool ANALYTIC, class FG>
+__device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, const LbOpts o) {
 #pragma clang fp contract(off)
   using namespace lb;
-  const double tol = (ftol / kEpsMch) * kEpsMch;
+  const double tol = (o.ftol / kEpsMch) * kEpsMch;
+  const double lo = o.lo, hi = o.hi;
+  const bool has_lo = BOUNDED && lo > -__builtin_inf();
+  const bool has_hi = BOUNDED && hi < __builtin_inf();
+  const bool boxed = has_lo && has_hi;
   int nfev = 0, nit = 0, ifun = 0;
   bool have_pair = false, in_ls = false;
   double s_last = 0.0, y_last = 0.0, theta = 1.0;
+  if (BOUNDED) x0 = dmin(dmax(x0, lo), hi);
   double x = x0, f = 0.0, g = 0.0;
   double z = 0.0, d = 0.0, stp = 0.0, xk = 0.0, fold = 0.0, gold = 0.0, gdold = 0.0;
   double x_eval = x0;
@@ -230,33 +258,48 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, doubl
   double x_last = 0.0, f_last = 0.0, g_last = 0.0;
   Dcsrch ls;
   for (;;) {
-    // ---- the single evaluation site: f and forward-difference g at x_eval.
-    // scipy's ScalarFunction memoises the last point: a repeated x costs no
+    // ---- the single evaluation site: f and g at x_eval.  scipy's
+    // ScalarFunction memoises the last point: a repeated x costs no
     // evaluation (and no nfev).
     if (!(have_last && x_eval == x_last)) {
-      double h = eps;
-      if ((x_eval + h) - x_eval == 0.0)
-        h = kSqrtEps * (x_eval >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(x_eval));
-      const double x1 = x_eval + h;
-      double f0, f1;
-      fg(x_eval, x1, f0, f1);
-      nfev += 2;
+      if constexpr (ANALYTIC) {
+        double f0, g0;
+        fg(x_eval, f0, g0);
+        nfev += 1;
+        f_last = f0;
+        g_last = g0;
+      } else {
+        double h = o.eps;
+        if ((x_eval + h) - x_eval == 0.0)
+          h = kSqrtEps * (x_eval >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(x_eval));
+        if (BOUNDED) {
+          const double ld = x_eval - lo, ud = hi - x_eval;
+          const double xt = x_eval + h;
+          const bool fitting = fabs(h) <= dmax(ld, ud);
+          if ((xt < lo || xt > hi) && fitting) h = -h;
+          else if (!fitting) h = (ud >= ld) ? ud : -ld;
+        }
+        const double x1 = x_eval + h;
+        double f0, f1;
+        fg(x_eval, x1, f0, f1);
+        nfev += 2;
+        f_last = f0;
+        g_last = (f1 - f0) / (x1 - x_eval);
+      }
       have_last = true;
       x_last = x_eval;
-      f_last = f0;
-      g_last = (f1 - f0) / (x1 - x_eval);
     }
     x = x_eval;
     f = f_last;
     g = g_last;
 
     if (!in_ls) {
-      if (fabs(g) <= gtol) return LbfgsResult{x, f, 0, nfev, 0};
+      if (fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol) return LbfgsResult{x, f, 0, nfev, 0};
     } else {
       int task = ls.step(stp, f, g * d);
       if (task == 0) {
         ++ifun;
-        if (ifun - 1 < maxls) {
+        if (ifun - 1 < o.maxls) {
           x_eval = (stp == 1.0) ? z : stp * d + xk;
           continue;
         }
@@ -269,10 +312,10 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, doubl
         theta = 1.0;
       } else {
         ++nit;
-        if (fabs(g) <= gtol) return LbfgsResult{x, f, nit, nfev, 0};
+        if (fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol) return LbfgsResult{x, f, nit, nfev, 0};
         if ((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))
           return LbfgsResult{x, f, nit, nfev, 1};
-        if (nit >= maxiter || nfev > maxfun) return LbfgsResult{x, f, nit, nfev, 3};
+        if (nit >= o.maxiter || nfev > o.maxfun) return LbfgsResult{x, f, nit, nfev, 3};
         const double gd = g * d;
         const double r = g - gold;
         const double rr = r * r;
@@ -289,14 +332,35 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, doubl
     }
     // ---- next search direction and line-search start (restarts loop here)
     for (;;) {
-      if (have_pair) z = x + (-g) * (s_last / y_last);
-      else z = x + (1.0 / theta) * (-g);
+      double dtm;
+      if (have_pair) { dtm = s_last / y_last; z = x + (-g) * dtm; }
+      else { dtm = 1.0 / theta; z = x + dtm * (-g); }
+      if (BOUNDED && g != 0.0) {
+        // cauchy: the bound is the one breakpoint along -g
+        if (g > 0.0 && has_lo) { if (!(dtm < (x - lo) / g)) z = lo; }
+        else if (g < 0.0 && has_hi) { if (!(dtm < (hi - x) / (-g))) z = hi; }
+      }
       d = z - x;
       const double dnorm = sqrt(d * d);
-      stp = (nit == 0) ? dmin(1.0 / dnorm, kStpMax) : 1.0;
+      double stpmx = kStpMax;
+      if (BOUNDED) {
+        if (nit == 0) {
+          stpmx = 1.0;
+        } else if (d < 0.0 && has_lo) {
+          const double a2 = lo - x;
+          if (a2 >= 0.0) stpmx = 0.0;
+          else if (d * stpmx < a2) stpmx = a2 / d;
+        } else if (d > 0.0 && has_hi) {
+          const double a2 = hi - x;
+          if (a2 <= 0.0) stpmx = 0.0;
+          else if (d * stpmx > a2) stpmx = a2 / d;
+        }
+      }
+      stp = (nit == 0 && !boxed) ? dmin(1.0 / dnorm, stpmx) : 1.0;
       xk = x; fold = f; gold = g;
       gdold = g * d;
       if (gdold < 0.0) {
+        ls.stpmax = stpmx;
         ls.start(stp, f, gdold);
         ifun = 1;
         in_ls = true;
@@ -308,6 +372,12 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0, doubl
       theta = 1.0;
     }
   }
+}
+
+// the reference's unbounded call (nem_order_mcmc.py:167)
+template <class FG>
+__device__ __forceinline__ LbfgsResult lbfgsb1_minimize(FG& fg, double x0) {
+  return lbfgsb1_minimize_opts<false, false>(fg, x0, LbOpts{});
 }
 
 }  // namespace nemo

@@ -127,7 +127,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
-                  c.d_fpartial, c.d_B8};
+                  c.d_fpartial, c.d_B8, c.d_inv_list};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -649,6 +649,211 @@ int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
   HIPCHK(hipMemcpyAsync(ow_out, c.d_ow + (size_t)chain * n, n * 8, hipMemcpyDeviceToHost, c.stream));
   HIPCHK(hipStreamSynchronize(c.stream));
   return NEMO_OK;
+}
+
+// ---------------------------------------------------------------------------
+// fixed-order optimizers (methods.py)
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// order_arr (utils.py:173-188) arranges a matrix by argsort(order) = pos:
+// row/column a of M is node pos[a], so node i sits at index perm[i].
+// InverseMethod.opt_b's loop (methods.py:125-127) visits, for i = 0..S-1,
+// k = order[0 .. pos[i]-1].  Pair (i, k) moves M[a][b], a = perm[i],
+// b = perm[k]; only a > b is inside the lower triangle solve_triangular
+// reads.  Its objective reads B[a][b], i.e. the entries M[r][c] with
+// b ~> c and r ~> a in the graph of lower-triangle pairs (~> : reachable,
+// reflexive).  Levels: a pair goes after every earlier pair it reads and no
+// earlier than any earlier pair that reads it (those must see its old
+// value; a level reads before it commits).  One level = one launch.
+void build_inverse_schedule(Ctx& c, int nprob, const int32_t* pos) {
+  const int S = c.S;
+  const size_t n = (size_t)nprob * S;
+  if (c.inv_pos.size() == n && memcmp(c.inv_pos.data(), pos, n * 4) == 0) return;
+  c.inv_pos.assign(pos, pos + n);
+  std::vector<std::vector<int32_t>> levels;
+  c.inv_skip.clear();
+  const int W = (S + 63) / 64;
+  for (int b = 0; b < nprob; ++b) {
+    const int32_t* pb = pos + (size_t)b * S;
+    std::vector<int> perm(S);
+    for (int i = 0; i < S; ++i) perm[pb[i]] = i;
+    // pairs in loop order
+    std::vector<int> pa, pbb, pi, pk;
+    for (int i = 0; i < S; ++i)
+      for (int p = 0; p < pb[i]; ++p) {
+        const int k = perm[p];
+        const int ra = perm[i], rb = perm[k];
+        const int32_t ent = (b << 16) | (i << 8) | k;
+        if (ra > rb) {
+          pa.push_back(ra);
+          pbb.push_back(rb);
+          pi.push_back(ent);
+        } else {
+          c.inv_skip.push_back(ent);
+        }
+      }
+    // reach[x] bitset of y with y ~> x
+    std::vector<uint64_t> reach((size_t)S * W, 0ull);
+    std::vector<char> edge((size_t)S * S, 0);
+    for (size_t q = 0; q < pa.size(); ++q) edge[(size_t)pa[q] * S + pbb[q]] = 1;
+    for (int x = 0; x < S; ++x) {
+      uint64_t* rx = &reach[(size_t)x * W];
+      rx[x >> 6] |= 1ull << (x & 63);
+      for (int d = 0; d < x; ++d)
+        if (edge[(size_t)x * S + d])
+          for (int w = 0; w < W; ++w) rx[w] |= reach[(size_t)d * W + w];
+    }
+    auto r = [&](int x, int y) { return (reach[(size_t)x * W + (y >> 6)] >> (y & 63)) & 1ull; };
+    const size_t P = pa.size();
+    std::vector<int> lev(P, 0);
+    for (size_t p = 0; p < P; ++p) {
+      const int a2 = pa[p], b2 = pbb[p];
+      int l = 0;
+      for (size_t q = 0; q < p; ++q) {
+        const int a1 = pa[q], b1 = pbb[q];
+        if (r(b1, b2) && r(a2, a1)) l = std::max(l, lev[q] + 1);  // p reads q
+        if (r(b2, b1) && r(a1, a2)) l = std::max(l, lev[q]);      // q reads p
+      }
+      lev[p] = l;
+      if ((int)levels.size() <= l) levels.resize(l + 1);
+      levels[l].push_back(pi[p]);
+    }
+  }
+  c.inv_list.clear();
+  c.inv_level_off.assign(1, 0);
+  for (auto& lv : levels) {
+    c.inv_list.insert(c.inv_list.end(), lv.begin(), lv.end());
+    c.inv_level_off.push_back((int)c.inv_list.size());
+  }
+}
+
+int opt_status(const Ctx& c, const std::vector<int32_t>& inf, int nprob) {
+  const size_t S = c.S;
+  for (size_t k = 0; k < inf.size(); ++k) {
+    if (inf[k] == -1) continue;  // not a permissible pair
+    const int status = inf[k] & 15;
+    if (status >= NEMO_LBFGSB_ABNORMAL) {
+      const size_t b = k / (S * S), i = (k / S) % S, j = k % S;
+      return fail(NEMO_ERR_OPT, "Minimization not successful, Reason: %s (problem %zu, pair %zu<-%zu)",
+                  status == NEMO_LBFGSB_ABNORMAL ? "ABNORMAL_TERMINATION_IN_LNSRCH"
+                                                 : "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT",
+                  b, i, j);
+    }
+  }
+  (void)nprob;
+  return NEMO_OK;
+}
+
+// eval with order weights of nprob problems on device weights d_w (cap 0 or
+// a cap), into c.d_ll and c.d_ow; leaves prep's pair lists in c.d_pairs
+int eval_with_ow(Ctx& c, int nprob, int cap, const double* d_w, hipStream_t st) {
+  HIPCHK(nemo::launch_prep(c, nprob, cap, c.d_pos, d_w, c.d_rows, c.d_sw, c.d_cnt, c.d_pairs, st));
+  if (c.score_path != 1 && c.factored)
+    HIPCHK(nemo::launch_score_factored(c, nprob, cap, c.d_pos, d_w, c.d_ll, nullptr, nullptr, c.d_ow, st));
+  else
+    HIPCHK(nemo::launch_score(c, nprob, c.d_rows, c.d_sw, c.d_cnt, c.d_ll, nullptr, nullptr, c.d_ow, st));
+  c.ow_chains = nprob;
+  return NEMO_OK;
+}
+
+int methods_prologue(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (nprob < 0) return fail(NEMO_ERR_ARG, "nprob=%d", nprob);
+  if (nprob > 0 && (!pos || !w)) return fail(NEMO_ERR_ARG, "null host pointer");
+  if (nprob > 32767) return fail(NEMO_ERR_ARG, "nprob=%d > 32767", nprob);
+  if (c.E > 80 * 64) return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by local optima", c.E);
+  if ((rc = check_pos(pos, nprob, c.S))) return rc;
+  if ((rc = nemo_reserve(ctx, nprob, nprob))) return rc;
+  const size_t S = c.S;
+  HIPCHK(hipMemcpyAsync(c.d_pos, pos, nprob * S * 4, hipMemcpyHostToDevice, c.stream));
+  HIPCHK(hipMemcpyAsync(c.d_wnew, w, nprob * S * S * 8, hipMemcpyHostToDevice, c.stream));
+  HIPCHK(hipMemsetAsync(c.d_info, 0xff, nprob * S * S * 4, c.stream));
+  return NEMO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nemo_gamma_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, int cap,
+                     double* w_out, double* ll_out, int32_t* info) {
+  int rc = methods_prologue(ctx, nprob, pos, w);
+  if (rc || nprob == 0) return rc;
+  if (cap < 0) return fail(NEMO_ERR_ARG, "cap=%d", cap);
+  if (!w_out || !ll_out) return fail(NEMO_ERR_ARG, "null host pointer");
+  Ctx& c = ctx->c;
+  const size_t S = c.S;
+  hipStream_t st = c.stream;
+  // opt_gamma: the evaluation takes the raw weights (methods.py:398)
+  HIPCHK(hipMemcpyAsync(c.d_w01, c.d_wnew, nprob * S * S * 8, hipMemcpyDeviceToDevice, st));
+  if ((rc = eval_with_ow(c, nprob, cap, c.d_w01, st))) return rc;
+  HIPCHK(nemo::launch_gamma_pairs(c, nprob, nemo::pairs_per_chain(c.S, cap), c.d_pairs, c.d_rows, c.d_w01,
+                                  c.d_ow, c.d_wnew, c.d_info, st));
+  std::vector<int32_t> inf((size_t)nprob * S * S);
+  HIPCHK(hipMemcpyAsync(w_out, c.d_wnew, nprob * S * S * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ll_out, c.d_ll, nprob * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(inf.data(), c.d_info, inf.size() * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (info) memcpy(info, inf.data(), inf.size() * 4);
+  return opt_status(c, inf, nprob);
+}
+
+int nemo_inverse_ancestral(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, double* out) {
+  int rc = methods_prologue(ctx, nprob, pos, w);
+  if (rc || nprob == 0) return rc;
+  if (!out) return fail(NEMO_ERR_ARG, "null host pointer");
+  Ctx& c = ctx->c;
+  const size_t S = c.S;
+  HIPCHK(nemo::launch_ancestral(c, nprob, c.d_pos, c.d_wnew, c.d_w01, c.stream));
+  HIPCHK(hipMemcpyAsync(out, c.d_w01, nprob * S * S * 8, hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  return NEMO_OK;
+}
+
+int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, double* w_out,
+                       double* ll_out, int32_t* info) {
+  int rc = methods_prologue(ctx, nprob, pos, w);
+  if (rc || nprob == 0) return rc;
+  if (!w_out || !ll_out) return fail(NEMO_ERR_ARG, "null host pointer");
+  Ctx& c = ctx->c;
+  const size_t S = c.S;
+  hipStream_t st = c.stream;
+  build_inverse_schedule(c, nprob, pos);
+  if (c.inv_list.size() > c.inv_list_cap) {
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(dalloc(&c.d_inv_list, c.inv_list.size()));
+    c.inv_list_cap = c.inv_list.size();
+  }
+  if (!c.inv_list.empty())
+    HIPCHK(hipMemcpyAsync(c.d_inv_list, c.inv_list.data(), c.inv_list.size() * 4, hipMemcpyHostToDevice, st));
+  // evaluation weights B/(1+B) (methods.py:118-121), evaluation (:122-123)
+  HIPCHK(nemo::launch_ancestral(c, nprob, c.d_pos, c.d_wnew, c.d_w01, st));
+  if ((rc = eval_with_ow(c, nprob, 0, c.d_w01, st))) return rc;
+  // the pair loop (:125-127), level by level, optima committed into d_wnew
+  for (size_t l = 0; l + 1 < c.inv_level_off.size(); ++l) {
+    const int o0 = c.inv_level_off[l], o1 = c.inv_level_off[l + 1];
+    HIPCHK(nemo::launch_inverse_level(c, o1 - o0, c.d_inv_list + o0, c.d_pos, c.d_wnew, c.d_ow, c.d_wdag,
+                                      c.d_info, st));
+  }
+  std::vector<int32_t> inf((size_t)nprob * S * S);
+  HIPCHK(hipMemcpyAsync(w_out, c.d_wnew, nprob * S * S * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ll_out, c.d_ll, nprob * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(inf.data(), c.d_info, inf.size() * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // pairs outside the lower triangle: B[a][b] = 0 whatever x, so the
+  // objective is flat and L-BFGS-B stops at the clipped start (nit 0, 2 f-evals)
+  for (int32_t ent : c.inv_skip) {
+    const size_t idx = ((size_t)(ent >> 16) * S + ((ent >> 8) & 0xff)) * S + (ent & 0xff);
+    w_out[idx] = std::min(std::max(w[idx], -5000.0), 500.0);
+    inf[idx] = NEMO_LBFGSB_CONV_PGTOL | (2 << 16);
+  }
+  if (info) memcpy(info, inf.data(), inf.size() * 4);
+  return opt_status(c, inf, nprob);
 }
 
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {

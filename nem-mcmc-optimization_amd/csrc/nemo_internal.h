@@ -70,6 +70,14 @@ struct Ctx {
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
   uint8_t* d_B8 = nullptr;         // [ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
 
+  // InverseMethod pair schedule (levels), cached per batch of orders
+  std::vector<int32_t> inv_pos;    // the orders the schedule was built for
+  std::vector<int32_t> inv_list;   // pair entries, level by level
+  std::vector<int> inv_level_off;  // level l = inv_list[off[l] .. off[l+1])
+  std::vector<int32_t> inv_skip;   // permissible pairs outside the lower triangle
+  int32_t* d_inv_list = nullptr;
+  size_t inv_list_cap = 0;
+
   // grouped (reuse) evaluation scratch
   int cap_group_batch = 0;
   int32_t* d_grows = nullptr;
@@ -169,6 +177,16 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int
   for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, kWave);
   return s;
 }
+// fixed-order optimizers of methods.py (nemo_methods.hip)
+hipError_t launch_gamma_pairs(Ctx& c, int nprob, int npairs, const int32_t* d_pairs, const int32_t* d_rows,
+                              const double* d_w, const double* d_ow, double* d_wout, int32_t* d_info,
+                              hipStream_t st);
+hipError_t launch_ancestral(Ctx& c, int nprob, const int32_t* d_pos, const double* d_w, double* d_out,
+                            hipStream_t st);
+// one level of InverseMethod.opt_b's pair loop (list entries prob << 16 | i << 8 | k),
+// then the commit of the level's optima into d_w
+hipError_t launch_inverse_level(Ctx& c, int n, const int32_t* d_list, const int32_t* d_pos, double* d_w,
+                                const double* d_ow, double* d_xout, int32_t* d_info, hipStream_t st);
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st);

@@ -77,6 +77,18 @@ class Engine:
             cache[key] = eng
         return eng
 
+    @classmethod
+    def for_tables(cls, U, score_tables, device: int = 0, dtype: str = "f64") -> "Engine":
+        """Engine for the (U, score_tables) pair a caller of methods.py holds:
+        the model's cached engine, staged from D, when the tables are a NEM's
+        lazy tables and U is its U; else a new engine on the given tables."""
+        from .nem import ScoreTables
+        if isinstance(score_tables, ScoreTables):
+            nem = score_tables._nem
+            if score_tables.knockdown_mat is nem.observed_knockdown_mat and np.array_equal(U, nem.U):
+                return cls.for_nem(nem, device=device, dtype=dtype)
+        return cls(U, np.asarray(score_tables, dtype=np.float64), device=device, dtype=dtype)
+
     @property
     def handle(self):
         return self._ctx
@@ -160,6 +172,41 @@ class Engine:
             raise Exception(_lib.load().nemo_last_error().decode())
         check(rc)
         return w_new, ll1, lld, info
+
+    # -- fixed-order optimizers (methods.py) --------------------------------
+    def _sweep(self, fn, pos, w, *extra, raise_on_fail=True):
+        pos = i32(np.atleast_2d(pos))
+        n = pos.shape[0]
+        w = f64(w).reshape(n, self.S, self.S)
+        w_out = np.empty_like(w)
+        ll = np.empty(n)
+        info = np.empty((n, self.S, self.S), dtype=np.int32)
+        rc = fn(self._ctx, n, ptr(pos, _lib._i32p), ptr(w), *extra, ptr(w_out), ptr(ll),
+                ptr(info, _lib._i32p))
+        if rc == _lib.NEMO_ERR_OPT and raise_on_fail:
+            # the reference raises a plain Exception (methods.py:115, :394)
+            raise Exception(_lib.load().nemo_last_error().decode())
+        if rc != _lib.NEMO_ERR_OPT:
+            check(rc)
+        return w_out, ll, info
+
+    def gamma_sweep(self, pos, w, cap: int = 0, raise_on_fail=True):
+        """``Method.opt_γ`` (methods.py:397-405) per problem: (w_out, ll, info)."""
+        return self._sweep(_lib.load().nemo_gamma_sweep, pos, w, int(cap), raise_on_fail=raise_on_fail)
+
+    def inverse_sweep(self, pos, w, raise_on_fail=True):
+        """``InverseMethod.opt_b`` (methods.py:117-129) per problem: (w_out, ll, info)."""
+        return self._sweep(_lib.load().nemo_inverse_sweep, pos, w, raise_on_fail=raise_on_fail)
+
+    def inverse_ancestral(self, pos, w):
+        """unorder_arr(order, B/(1+B)), B = (I - order_arr(order, exp(w)))^-1 lower
+        (methods.py:118-121, :160-164), per problem."""
+        pos = i32(np.atleast_2d(pos))
+        n = pos.shape[0]
+        w = f64(w).reshape(n, self.S, self.S)
+        out = np.empty_like(w)
+        check(_lib.load().nemo_inverse_ancestral(self._ctx, n, ptr(pos, _lib._i32p), ptr(w), ptr(out)))
+        return out
 
     def order_weights(self, chain: int = 0) -> np.ndarray:
         out = np.empty((self.S + 1, self.E))

@@ -190,29 +190,56 @@ class Dcsrch:
         return stp, "FG"
 
 
-def minimize_1d(fun, x0, ftol=0.01, gtol=0.01, eps=1e-8, maxls=20, maxiter=15000, maxfun=15000):
-    """Returns (x*, f*, nit, nfev, status)."""
+def minimize_1d(fun, x0, ftol=0.01, gtol=0.01, eps=1e-8, maxls=20, maxiter=15000, maxfun=15000,
+                lo=-math.inf, hi=math.inf, jac=False):
+    """Returns (x*, f*, nit, nfev, status).
+
+    ``lo``/``hi``: the bounds (scipy ``bounds=[(lo, hi)]``); ``jac=True``:
+    ``fun`` returns (f, g) (scipy ``jac=True``), else forward differences with
+    absolute step ``eps``.  With both bounds finite (the fixed-order methods,
+    methods.py:95, :238, :384) L-BFGS-B 3.0 runs its constrained branch:
+    x0 clipped, projected gradient, generalised Cauchy point with the bound
+    as breakpoint, unit first step and stpmax from the bounds."""
     nfev = 0
     cache = [None, 0.0, 0.0]   # scipy's ScalarFunction memoises the last (x, f, g)
+    cnstnd = lo > -math.inf or hi < math.inf
+    boxed = lo > -math.inf and hi < math.inf
 
     def f_and_g(x):
         nonlocal nfev
         if cache[0] is not None and x == cache[0]:
             return cache[1], cache[2]
-        f0 = fun(x)
-        h = eps
-        if (x + h) - x == 0.0:
-            h = SQRT_EPS * (1.0 if x >= 0.0 else -1.0) * max(1.0, abs(x))
-        x1 = x + h
-        g = (fun(x1) - f0) / (x1 - x)
-        nfev += 2
+        if jac:
+            f0, g = fun(x)
+            nfev += 1
+        else:
+            f0 = fun(x)
+            h = eps
+            if (x + h) - x == 0.0:
+                h = SQRT_EPS * (1.0 if x >= 0.0 else -1.0) * max(1.0, abs(x))
+            if cnstnd:     # scipy optimize/_numdiff.py _adjust_scheme_to_bounds('1-sided')
+                ldist, udist = x - lo, hi - x
+                xt = x + h
+                fitting = abs(h) <= max(ldist, udist)
+                if (xt < lo or xt > hi) and fitting:
+                    h = -h
+                elif not fitting:
+                    h = udist if udist >= ldist else -ldist
+            x1 = x + h
+            g = (fun(x1) - f0) / (x1 - x)
+            nfev += 2
         cache[:] = [x, f0, g]
         return f0, g
 
+    def projg(x, g):           # projgr
+        if g < 0.0:
+            return max(x - hi, g) if hi < math.inf else g
+        return min(x - lo, g) if lo > -math.inf else g
+
     tol = (ftol / EPSMCH) * EPSMCH
-    x = float(x0)
+    x = min(max(float(x0), lo), hi)
     f, g = f_and_g(x)
-    if abs(g) <= gtol:
+    if abs(projg(x, g)) <= gtol:
         return x, f, 0, nfev, CONV_PGTOL
     nit = 0
     have_pair = False   # col > 0
@@ -222,20 +249,49 @@ def minimize_1d(fun, x0, ftol=0.01, gtol=0.01, eps=1e-8, maxls=20, maxiter=15000
         # search direction d = z - x, z the subspace minimiser (lnsrlb works
         # with the rounded d, and evaluates the unit step at z itself):
         # Cauchy point x - g/theta before the first update (theta = 1 then),
-        # secant-Newton step -g*s/y afterwards (all variables free)
+        # secant-Newton step -g*s/y afterwards; with bounds, the GCP stops at
+        # the bound when the model's minimiser lies beyond it (cauchy: the
+        # breakpoint tl/g or tu/-g against dtm)
         if have_pair:
-            z = x + (-g) * (s_last / y_last)
+            dtm = s_last / y_last
+            z = x + (-g) * dtm
         else:
-            z = x + (1.0 / theta) * (-g)
+            dtm = 1.0 / theta
+            z = x + dtm * (-g)
+        if cnstnd and g != 0.0:
+            if g > 0.0 and lo > -math.inf:
+                dt, zb = (x - lo) / g, lo
+            elif g < 0.0 and hi < math.inf:
+                dt, zb = (hi - x) / (-g), hi
+            else:
+                dt = None
+            if dt is not None and not (dtm < dt):
+                z = zb
         d = z - x
         # lnsrlb
         dnorm = math.sqrt(d * d)
-        stp = min(1.0 / dnorm, 1e10) if nit == 0 else 1.0
+        stpmx = 1e10
+        if cnstnd:
+            if nit == 0:
+                stpmx = 1.0
+            elif d < 0.0 and lo > -math.inf:
+                a2 = lo - x
+                if a2 >= 0.0:
+                    stpmx = 0.0
+                elif d * stpmx < a2:
+                    stpmx = a2 / d
+            elif d > 0.0 and hi < math.inf:
+                a2 = hi - x
+                if a2 <= 0.0:
+                    stpmx = 0.0
+                elif d * stpmx > a2:
+                    stpmx = a2 / d
+        stp = min(1.0 / dnorm, stpmx) if (nit == 0 and not boxed) else 1.0
         xk, fold, gold = x, f, g
         gd = g * d
         task = "FAIL"
         if gd < 0.0:
-            ls = Dcsrch(0.0, 1e10)
+            ls = Dcsrch(0.0, stpmx)
             stp, task = ls.start(stp, f, gd)
             gdold = gd
             ifun = 0
@@ -260,7 +316,7 @@ def minimize_1d(fun, x0, ftol=0.01, gtol=0.01, eps=1e-8, maxls=20, maxiter=15000
             theta = 1.0
             continue
         nit += 1
-        if abs(g) <= gtol:
+        if abs(projg(x, g)) <= gtol:
             return x, f, nit, nfev, CONV_PGTOL
         if (fold - f) <= tol * max(abs(fold), abs(f), 1.0):
             return x, f, nit, nfev, CONV_REL

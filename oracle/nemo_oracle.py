@@ -139,6 +139,83 @@ def local_optimum(c, x_anc, x0):
 
 
 # --------------------------------------------------------------------------
+# 8(f) rank 2 -- fixed-order optimizers (methods.py)
+# --------------------------------------------------------------------------
+def order_arr(order, a):
+    """utils.py:173-188: every axis permuted by argsort(order)."""
+    idx = np.argsort(order)
+    return a[np.ix_(idx, idx)]
+
+
+def unorder_arr(order, a):
+    """utils.py:190-216: inverse of order_arr."""
+    inv_idx = np.argsort(np.argsort(order))
+    return a[np.ix_(inv_idx, inv_idx)]
+
+
+def local_ll_sum_gamma(g, c):
+    """methods.py:8-9 (value and gradient)."""
+    return (-np.sum(np.log(g * c + 1.0)), -np.sum(c / (g * c + 1.0)))
+
+
+def opt_gamma(u, t, order, weights):
+    """Method.opt_γ (methods.py:397-405, local optimum :385-395) -> (ll, new
+    weights); raises like the reference when a minimisation fails."""
+    parents = parents_of(order)
+    ow, ll, _ = calculate_ll(cell_ratios(u, t, parents, weights))
+    new = np.array(weights, dtype=np.float64, copy=True)
+    for i in range(t.shape[0]):
+        for k in parents[i]:
+            lv = np.exp(t[i][k])
+            a = (lv - 1.0) * ow[k]
+            b = 1.0 - new[i][k] * a + new[i][k] * (lv - 1.0)
+            c = a / b
+            res = minimize(local_ll_sum_gamma, x0=new[i][k], bounds=[(0, 1)], args=(c,), jac=True,
+                           method="L-BFGS-B", tol=0.01)
+            if res.success is False:
+                raise Exception(f"Minimization not successful, Reason: {res.message}")
+            new[i][k] = res.x[0]
+    return ll, new
+
+
+def _b_inv(order, weights, eye):
+    """B / (1 + B) of B = solve_triangular(I - order_arr(exp(W)), I, lower=True), unordered."""
+    from scipy.linalg import solve_triangular
+    w = order_arr(order, np.exp(weights))
+    b = solve_triangular(eye - w, eye, lower=True)
+    return unorder_arr(order, b / (1.0 + b))
+
+
+def local_ll_sum_b_inv(x, weights, i, k, local_vec, a_vec, order, eye):
+    """methods.py:73-82 (writes x into weights[i][k], as the reference does)."""
+    weights[i][k] = np.asarray(x).ravel()[0]
+    bik = _b_inv(order, weights, eye)[i][k]
+    b_vec = 1.0 - bik * a_vec + bik * (local_vec - 1.0)
+    c_vec = a_vec / b_vec
+    return -np.sum(np.log(bik * c_vec + 1.0))
+
+
+def opt_b(u, t, order, weights):
+    """InverseMethod.opt_b (methods.py:117-129, local optimum :106-115) ->
+    (ll, new weights); the pair loop updates the weights in place."""
+    s = t.shape[0]
+    eye = np.eye(s)
+    parents = parents_of(order)
+    ow, ll, _ = calculate_ll(cell_ratios(u, t, parents, _b_inv(order, weights, eye)))
+    new = np.array(weights, dtype=np.float64, copy=True)
+    for i in range(s):
+        for k in parents[i]:
+            lv = np.exp(t[i][k])
+            a_vec = (lv - 1.0) * ow[i]
+            res = minimize(local_ll_sum_b_inv, x0=new[i][k], bounds=[(-5000, 500)], options={"eps": 1e-3},
+                           args=(new, i, k, lv, a_vec, order, eye), method="L-BFGS-B", tol=0.1)
+            if res.success is False:
+                raise Exception(f"Minimization not successful, Reason: {res.message}")
+            new[i][k] = res.x[0]
+    return ll, new
+
+
+# --------------------------------------------------------------------------
 # A6/A7/A9 -- sampler (nem_order_mcmc.py:29-310)
 # --------------------------------------------------------------------------
 class OracleSampler:

@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -225,6 +225,46 @@ def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=
     print("replica exchange:", best_score, [r["n_ex"] for r in rounds])
 
 
+def capture_methods(ref_nem, ref_utils, gen):
+    """The fixed-order optimizers of methods.py:
+    ``Method.optimize`` (methods.py:407-436) and ``InverseMethod.optimize``
+    (:131-172) on net2 and C2 from the initial order guess.  Recorded per
+    weight sweep (opt_gamma :397-405 / opt_b :117-129): the sweep's ll and
+    the weights it returns; and the optimizers' outputs."""
+    import methods as ref_methods
+    out = {}
+    adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
+    m2 = quiet(ref_nem.NEM, adj, end, err, s, e)
+    net = gen.synthetic_network(16, 500, 0)
+    mc2 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 16, 500)
+    for name, m, iters in (("net2", m2, {"gamma": 1000, "inverse": 1000}),
+                           ("C2", mc2, {"gamma": 60, "inverse": 1000})):
+        tables = m.get_score_tables(m.observed_knockdown_mat)
+        order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+        for kind, cls, sweep in (("gamma", ref_methods.Method, "opt_γ"),
+                                 ("inverse", ref_methods.InverseMethod, "opt_b")):
+            meth = cls(order, m.num_s, m.num_e, m.U, tables)
+            lls, ws = [], []
+            orig = getattr(meth, sweep)
+
+            def rec(weights, bounds, orig=orig, lls=lls, ws=ws):
+                ll, w = orig(weights, bounds)
+                lls.append(ll)
+                ws.append(np.array(w, dtype=np.float64))
+                return ll, w
+            setattr(meth, sweep, rec)
+            dag, real_ll = quiet(meth.optimize, max_iter=iters[kind])
+            keep = min(len(ws), 40)
+            np.savez_compressed(
+                os.path.join(HERE, f"methods_{kind}_{name}.npz"), S=m.num_s, E=m.num_e, order=order,
+                D=m.observed_knockdown_mat.astype(np.uint8), A=m.A, B=m.B, max_iter=iters[kind],
+                sweep_ll=np.array(lls), sweep_w=np.array(ws[:keep]), last_w=ws[-1],
+                dag=np.asarray(dag), real_ll=real_ll)
+            out[(name, kind)] = (len(lls), real_ll)
+            print(name, kind, "sweeps", len(lls), "real_ll", real_ll, flush=True)
+    return out
+
+
 def main():
     import scipy
     ref_nem, ref_mcmc, ref_utils = load_reference()
@@ -232,6 +272,9 @@ def main():
         capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
         return
     gen = repo_generator()
+    if "--only-methods" in sys.argv:
+        capture_methods(ref_nem, ref_utils, gen)
+        return
 
     # KAT from the reference's own test (tests/utils.tests.py:11-27): data only.
     s_mat = np.array([[0, 1, 1, 0, 1, 0], [0, 0, 1, 0, 1, 0], [0, 0, 0, 0, 1, 0],
@@ -279,6 +322,7 @@ def main():
     capture_traj(ref_mcmc, mc2, order2, 2.0 * 16 / 500, 0.95, 20, "C2_20", record_local_every=7)
 
     capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
+    capture_methods(ref_nem, ref_utils, gen)
 
     meta = dict(python=platform.python_version(), numpy=np.__version__, scipy=scipy.__version__,
                 machine=platform.machine(), processor=platform.processor(), reference=REF)
