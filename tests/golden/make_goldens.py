@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -265,9 +265,68 @@ def capture_methods(ref_nem, ref_utils, gen):
     return out
 
 
+def capture_networks(ref_nem, ref_mcmc, ref_utils, n_iter=10):
+    """The bundled networks 0-19 (DAGs/networks).
+    Copies each network's data files (closure CSV, reduced CSV and the DOT
+    files the reference's DAGs/dot.py:4-26 made from them) into
+    ``networks/``, and records per network a short run of main.py's MCMC
+    configuration (initial_order_guess, gamma = 2S/E, swap_prob 0.90,
+    main.py:62-70) with the DOT text output_handling (main.py:44-53) writes
+    for the best DAG (DAGs/dot.py:28-42)."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.join(REF, "DAGs"))
+    import dot as ref_dot
+    dst = os.path.join(HERE, "networks")
+    os.makedirs(dst, exist_ok=True)
+    out = {}
+    for i in range(20):
+        base = os.path.join(REF, f"DAGs/networks/network{i}/network{i}")
+        for suffix in (".csv", ".dot", "_red.csv", "_red.dot"):
+            shutil.copyfile(base + suffix, os.path.join(dst, f"network{i}{suffix}"))
+        adj, end, err, s, e = ref_utils.read_csv_to_adj(base + ".csv")
+        m = ref_nem_without_diagnostics(ref_nem, ref_utils, adj, end, err, s, e)
+        order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+        acc = []
+        cls = ref_mcmc.NEMOrderMCMC
+        orig_acc = cls.accepting
+
+        def accepting(self, *a, orig_acc=orig_acc, acc=acc):
+            r = orig_acc(self, *a)
+            acc.append(bool(r[0]))
+            return r
+        cls.accepting = accepting
+        try:
+            mc = cls(m, order)
+            best, best_dag = quiet(mc.method, n_iterations=n_iter, gamma=2.0 * s / e, swap_prob=0.90)
+        finally:
+            cls.accepting = orig_acc
+        texts = []
+        cwd = os.getcwd()
+        with tempfile.TemporaryDirectory() as td:
+            os.makedirs(os.path.join(td, "x"))
+            for k, mat in enumerate((ref_utils.ancestor(best_dag), ref_utils.transitive_reduction(best_dag))):
+                os.chdir(os.path.join(td, "x"))  # generate_dot_from_matrix changes directory to '../'
+                path = os.path.join(td, f"o{k}.dot")
+                quiet(ref_dot.generate_dot_from_matrix, mat, path)
+                with open(path) as fh:
+                    texts.append(fh.read())
+        os.chdir(cwd)
+        out.update({f"n{i}_order0": np.asarray(order), f"n{i}_all_scores": np.array(mc.all_score_list),
+                    f"n{i}_acc": np.array(acc), f"n{i}_best_score": best,
+                    f"n{i}_best_order": np.asarray(mc.best_order), f"n{i}_best_dag": np.asarray(best_dag),
+                    f"n{i}_closed_dot": np.array(texts[0]), f"n{i}_red_dot": np.array(texts[1]),
+                    f"n{i}_D_packed": np.packbits(m.observed_knockdown_mat.astype(np.uint8), axis=None)})
+        print(f"network{i}: S={s} E={e} best={best} accepts={sum(acc)}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "networks_mcmc.npz"), n_iter=n_iter, **out)
+
+
 def main():
     import scipy
     ref_nem, ref_mcmc, ref_utils = load_reference()
+    if "--only-networks" in sys.argv:
+        capture_networks(ref_nem, ref_mcmc, ref_utils)
+        return
     if "--only-replica" in sys.argv:
         capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
         return
@@ -323,6 +382,7 @@ def main():
 
     capture_replica_exchange(ref_nem, ref_mcmc, ref_utils)
     capture_methods(ref_nem, ref_utils, gen)
+    capture_networks(ref_nem, ref_mcmc, ref_utils)
 
     meta = dict(python=platform.python_version(), numpy=np.__version__, scipy=scipy.__version__,
                 machine=platform.machine(), processor=platform.processor(), reference=REF)
