@@ -172,8 +172,14 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                int8 fixed-point factored kernel, the rest the chunked fp64
  *                one; 1 = chunked; 2 / 3 = fp64 pipelined with 4 / 8 waves
  *                per block; 4 / 5 = int8 with 4 / 5 digit pairs; 6 = int8
- *                with 8 waves per block
- *   "factored"   (get only) 1 if the staged table is factorable */
+ *                with 8 waves per block; 7 / 8 = int8 with the offset
+ *                log-sum-exp (4 / 8 waves), which auto prefers when the
+ *                staged model passes its range checks (option "i8o")
+ *   "factored"   (get only) 1 if the staged table is factorable
+ *   "i8o"        (get only) 0: no offset int8 kernel for this model; 1: it
+ *                reads U - U[S] per cell; 2: U - U[S] is two-valued per row
+ *                and rides in the contraction (no U reads)
+ *   "i8o_nodiag" 1 = keep the U reads even when 2 is available (testing) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

@@ -127,7 +127,8 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
-                  c.d_fpartial, c.d_B8, c.d_inv_list};
+                  c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
+                  c.d_udig, c.d_u0};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -209,6 +210,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
   const size_t S = c.S, E = c.E;
   const int nwords = (int)((E + 63) / 64);
   c.factored = fact;
+  c.i8o_ok = false;
   c.fspad = nemo::factored_spad(c.S);
   c.nwords = nwords;
   if (fact) {
@@ -243,6 +245,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
       HIPCHK(hipMalloc((void**)&c.d_B8, b8.size()));
       HIPCHK(hipMemcpy(c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
     }
+    HIPCHK(nemo::stage_i8o(c, elo, ehi, d1));
   }
   // grow the factored scratch if a batch was reserved before staging
   if (c.cap_batch > 0) {
@@ -865,8 +868,12 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 6) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..6", value);
+    if (value < 0 || value > 8) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..8", value);
     ctx->c.fact_kernel = value;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "i8o_nodiag") == 0) {
+    ctx->c.i8o_nodiag = value != 0;
     return NEMO_OK;
   }
   if (strcmp(name, "score_path") == 0) {
@@ -886,6 +893,8 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "score_path") == 0) *value = c.score_path;
   else if (strcmp(name, "factored") == 0) *value = c.factored ? 1 : 0;
   else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
+  else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
+  else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;
 }

@@ -545,18 +545,26 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   }
   // option fact_kernel: 0 auto (kAutoFactKernel for ll-only calls with
   // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,
-  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves
+  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves,
+  // 7 / 8 int8 with the offset log-sum-exp (4 / 8 waves); auto prefers 7/8
   const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool ll_only = !d_cs && !d_cells && !d_ow;
   const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
   const bool i8 = spad <= 64 && fk >= 4 && ll_only && c.d_B8;
   int np = 0;
   bool finalized = false;
-  if (i8) {
+  const bool i8o = i8 && c.i8o_ok && (fk == 7 || fk == 8 || c.fact_kernel == 0);
+  if (i8o) {
+    // 7 / 8: offset log-sum-exp with 4 / 8 waves per block (auto: 8)
+    const int waves = fk == 7 ? 4 : 8;
+    err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, st, &np, &finalized);
+  } else if (i8 && fk <= 6) {
     // auto: 4 waves per block for large batches, 8 (fewer splits) below
     const int waves = fk == 6 ? 8 : (fk == 4 && c.fact_kernel == 0 && batch < 384 ? 8 : 4);
     err = launch_score_i8(c, batch, cap, d_pos, d_w01, d_ll, fk == 5 ? 5 : 4, waves, st, &np,
                           &finalized);
+  } else if (i8) {
+    return hipErrorInvalidValue;  // 7 / 8 asked for but the staging bounds do not hold
   } else if (pipe) {
     const bool w8 = fk == 3;
     switch (spad / 16) {

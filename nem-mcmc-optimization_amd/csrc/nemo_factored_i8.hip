@@ -26,6 +26,12 @@
 
 #include <math.h>
 
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 #ifndef NEMO_I8_ABLATE
 #define NEMO_I8_ABLATE 0
 #endif
@@ -97,13 +103,13 @@ struct EvalLds {
 // perm from pos, G preset (0 / kPadG8 on padding rows), digits zeroed
 template <int SPAD, int NSL>
 __device__ __forceinline__ void i8_init_eval(EvalLds e, const int32_t* __restrict__ pb, int S, int tid,
-                                             int nthreads) {
+                                             int nthreads, double padg = kPadG8) {
   for (int j = tid; j < S; j += nthreads) {
     int pj = pb[j];
     pj = pj < 0 ? 0 : (pj >= S ? S - 1 : pj);  // malformed input must not fault
     e.perm[pj] = j;
   }
-  for (int i = tid; i < SPAD; i += nthreads) e.G[i] = i < S ? 0.0 : kPadG8;
+  for (int i = tid; i < SPAD; i += nthreads) e.G[i] = i < S ? 0.0 : padg;
   for (int k = tid; k < NSL * SPAD * kARow; k += nthreads) e.A[k] = i32x4{0, 0, 0, 0};
 }
 
@@ -425,7 +431,412 @@ hipError_t launch_i8_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const d
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// score_i8o_kernel: the same contraction with an offset log-sum-exp.
+//
+// The column log-sum-exp needs SOME offset, not the maximum: with the null
+// row as the offset,
+//     cs[e] = U[S][e] + log(1 + sum_{i<S} exp(x[i][e])),
+//     x[i][e] = cell[i][e] - U[S][e] = U'[i][e] + G[i] + (Delta.D1)[i][e],
+// where U' = U - U[S] is staged once (stage_i8o).  Staging bounds |x| <= 690
+// for every order and weight in [0, 1] (each log factor lies between 0 and
+// T), so no exp overflows, the sum stays finite and no term is subnormal:
+// the exponent of 2^(k/256) goes straight into the table entry's exponent
+// field.  Against score_i8_kernel this drops the max pass and its two
+// cross-lane steps, the "- m" per cell, the ldexp and the null row's exp, and
+// each cell's exp is accumulated as soon as the cell exists, so no cell is
+// held (fewer registers, more waves per SIMD).  G rides in the integer
+// accumulators: G = g0 2^(c-24) + g1 2^(c-48) (+ <= 2^(c-49)), g0 / g1 the C
+// init of the pair-1 / pair-3 accumulators, so a cell is two cvt + two fma.
+// The column sum over the four row groups uses the gfx950 permlane swaps
+// (VALU, no LDS round trip).  Sums per set: sum_e U[S][e] is a staged
+// constant per 8-tile set (fixed order), the logs run once per set on
+// prod(l) kept as mantissa * 2^lexp.
+// ---------------------------------------------------------------------------
+#ifndef NEMO_I8O_WAVES_PER_SIMD
+#define NEMO_I8O_WAVES_PER_SIMD 4
+#endif
+
+// acc + e^x for |x| <= 700: 2^(k/2048) e^r, k = rint(x 2048/ln2), |r| <=
+// ln2/4096, degree-3 series (error r^4/24 < 4e-17).  The rounding constant is
+// 1.5 2^52 + kBias, kBias = 1023 * 2048, so the low dword of t is k + kBias
+// (> 0 for x > -709): its low 11 bits are the table index j = k & 2047 and
+// (lo << 9) = ((k >> 11) + 1023) << 20 + (j << 9).  The table entry's high
+// dword is stored as hi(2^(j/2048)) with its exponent field cleared, minus
+// (j << 9), so one shift-add makes the exponent field 1023 + (k >> 11) (no
+// ldexp; |x| <= 700 keeps it normal).  Table: kExpTabN entries, 16 KB.
+constexpr int kExpTabN = 2048;
+constexpr double kExpMagicB = 6755399441055744.0 + 1023.0 * 2048.0;
+
+__device__ __forceinline__ double exp_acc(double x, const uint2* __restrict__ tab, double acc) {
+  constexpr double kInvLn2x2048 = 2954.6394437405970166;
+  constexpr double kLn2d2048 = 3.3845077175778578e-04;
+  const double t = fma(x, kInvLn2x2048, kExpMagicB);
+  const double kf = t - kExpMagicB;
+  const uint32_t lo = (uint32_t)__builtin_bit_cast(uint64_t, t);
+  const double r = fma(-kf, kLn2d2048, x);
+  double p = fma(r, 1.0 / 6.0, 0.5);
+  p = fma(r, p, 1.0);
+  p = fma(r, p, 1.0);
+#if NEMO_I8_ABLATE & 64  // instrumented build: every lane reads entry 0 (no bank conflicts)
+  const uint2 e = tab[lo & 0u];
+#else
+  const uint2 e = tab[lo & (kExpTabN - 1)];
+#endif
+  const uint32_t hi = (lo << 9) + e.y;
+  return fma(p, __builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), acc);
+}
+
+// sum over the four 16-lane rows (lanes col, col+16, col+32, col+48), in
+// every lane: v_permlane16_swap then v_permlane32_swap (both outputs kept)
+__device__ __forceinline__ double rowsum4(double v) {
+  uint64_t b = __builtin_bit_cast(uint64_t, v);
+  auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  double a0 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  double a1 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  v = a0 + a1;
+  b = __builtin_bit_cast(uint64_t, v);
+  lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+  hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  a0 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  a1 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return a0 + a1;
+}
+
+template <int NR, int WAVES, bool DIAG>
+__global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8o_kernel(
+    int S, int E, int ntiles, int nsets, int split, int cap, int cexp, double padg,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const double* __restrict__ Uoff,
+    const int8_t* __restrict__ udig, const double* __restrict__ u0,
+    const double* __restrict__ nullsum, const void* __restrict__ tabs, double sA, double sB,
+    double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
+  constexpr int SPAD = NR * 16;
+  constexpr int NP = 4;
+  constexpr int NSL = 2 * NP;
+  extern __shared__ __attribute__((aligned(16))) double lds8[];
+  uint2* etab_o = (uint2*)lds8;                          // [kExpTabN] exp_acc's table
+  double2* ltab = (double2*)(etab_o + kExpTabN);         // [128] log table
+  double* elo_s = (double*)(ltab + 128);                 // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  EvalLds ev;
+  ev.G = ehi_s + SPAD;                                   // [SPAD]
+  int* gi = (int*)(ev.G + SPAD);                         // [2][SPAD] g0, g1
+  ev.perm = gi + 2 * SPAD;                               // [SPAD]
+  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][SPAD][kARow]
+
+  const int work = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / split;
+  const int part = work - b * split;
+  const int spb = (nsets + split - 1) / split;
+  const int s_begin = part * spb;
+  const int s_end = min(nsets, s_begin + spb);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int col = lane & 15, rg = lane >> 4;
+
+  {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    const int4* src = (const int4*)tabs;
+    int4* dst = (int4*)lds8;
+    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+  }
+  i8_init_eval<SPAD, NSL>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
+  __syncthreads();
+  if constexpr (DIAG) {  // U' as the free diagonal "parent" i of child i (stage_i8o)
+    int8_t* A8 = (int8_t*)ev.A;
+    for (int k = tid; k < S * NSL; k += blockDim.x) {
+      const int i = k / NSL, sl = k - i * NSL;
+      A8[(sl * SPAD + i) * (16 * kARow) + i] = udig[k];
+    }
+  }
+  {
+    constexpr int KB = 4;
+    const int npass = i8_npass(S, cap);
+    const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
+    for (int k0 = 0; k0 < my; k0 += KB)
+      i8_prep_passes<SPAD, NSL, WAVES, KB>(ev, k0, w, lane, S, cap, cexp, w01 + (size_t)b * S * S,
+                                           elo_s, ehi_s, ltab);
+  }
+  __syncthreads();
+  // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c))
+  for (int i = tid; i < SPAD; i += blockDim.x) {
+    const double g = DIAG && i < S ? ev.G[i] + u0[i] : ev.G[i];
+    const double g0 = rint(ldexp(g, 24 - cexp));
+    const double rho = fma(-g0, ldexp(1.0, cexp - 24), g);  // exact
+    gi[i] = (int)g0;
+    gi[SPAD + i] = (int)rint(ldexp(rho, 48 - cexp));
+  }
+  const uint32_t uln8 = (uint32_t)(4 * rg * E + col) * 8u;  // byte offset of this lane's U' cells
+  __syncthreads();
+#if NEMO_I8_ABLATE & 32  // instrumented build (tools/ablate.sh): prep only, no tiles
+  if (s_end > 0) return;
+#endif
+
+  const i32x4* Bt = (const i32x4*)B8;
+  const i32x4* Gi = (const i32x4*)gi;
+  const uint32_t a_lane = (uint32_t)(col * kARow + rg);
+  int set = s_begin + w;
+  if (set < s_end) {
+    double lprod = 1.0;
+    int lexp = 0;
+    double uc[NR][4];
+    int t = 8 * set;
+    // U' through a buffer resource: the lane offset stays in one VGPR, the
+    // tile and row offsets are scalar (no per-load address arithmetic)
+    const __amdgpu_buffer_rsrc_t urs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)Uoff, (short)0, (int)((SPAD + 1) * E + 16) * 8, 0x00020000);
+    auto uload = [&](int tt, int row) {
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                            urs, uln8, (tt * 16 + row * E) * 8, 0));
+    };
+    if constexpr (!DIAG)
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) uc[r][g] = uload(t, 16 * r + g);
+    i32x4 bc = Bt[(size_t)t * kWave + lane];
+    for (;;) {
+      uint32_t ao = a_lane;
+      asm volatile("" : "+v"(ao));
+      const i32x4* Al = ev.A + ao;
+      int tn = t + 1, setn = set;
+      if (tn >= min(ntiles, 8 * set + 8)) {
+        setn = set + WAVES;
+        tn = 8 * setn;
+      }
+      const bool more = setn < s_end;
+      const int tl = more ? tn : t;  // prefetch target (the current tile again at the end)
+      const i32x4 b1 = bc;
+      const i32x4 b64 = b1 << 6;
+      bc = Bt[(size_t)tl * kWave + lane];
+      double ls0 = 0.0, ls1 = 0.0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        i32x4 acc[NP];
+        const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+        const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+#pragma unroll
+        for (int pr = 0; pr < NP; ++pr) {
+          const i32x4 a0 = Al[((2 * pr) * SPAD + 16 * r) * kARow];
+          const i32x4 a1 = Al[((2 * pr + 1) * SPAD + 16 * r) * kARow];
+          const i32x4 ci = pr == 1 ? c0 : (pr == 3 ? c1 : i32x4{0, 0, 0, 0});
+          acc[pr] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b64, ci, 0, 0, 0);
+          acc[pr] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, acc[pr], 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ta = (acc[0][g] << 12) + acc[1][g];
+          const int tb = (acc[2][g] << 12) + acc[3][g];
+          double x;
+          if constexpr (DIAG) {
+            x = fma((double)ta, sA, (double)tb * sB);
+          } else {
+            x = fma((double)ta, sA, fma((double)tb, sB, uc[r][g]));
+            uc[r][g] = uload(tl, 16 * r + g);
+          }
+#if NEMO_I8_ABLATE & 1  // instrumented build: no exp
+          if (g & 1) ls1 += x;
+          else ls0 += x;
+#else
+          if (g & 1) ls1 = exp_acc(x, etab_o, ls1);
+          else ls0 = exp_acc(x, etab_o, ls0);
+#endif
+        }
+      }
+      double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
+      lprod *= t * 16 + col < E ? l : 1.0;
+      lexp += __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      if (setn != set) {  // set complete: one partial
+        double v = log(lprod) + (double)lexp * 0.69314718055994530942;
+        v = wsum(lane < 16 ? v : 0.0);
+        if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+        lprod = 1.0;
+        lexp = 0;
+      }
+      if (!more) break;
+      t = tn;
+      set = setn;
+    }
+  }
+  if (split == 1) {
+    __syncthreads();
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nsets, nsets, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
+}
+
+template <int NR, int WAVES, bool DIAG>
+hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                        double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  const int nsets = (ntiles + 7) / 8;
+  const int slots = 256 * (NEMO_I8O_WAVES_PER_SIMD * 4 / WAVES);
+  int split = (slots + batch - 1) / batch;
+  split = split < 1 ? 1 : (split > nsets ? nsets : split);
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)8 * SPAD * 16 * kARow;
+  const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48);
+  score_i8o_kernel<NR, WAVES, DIAG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi,
+      c.d_B8, c.d_Uoff, c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB, c.d_fpartial, d_ll,
+      c.xcd_remap);
+  *nparts = nsets;
+  *finalized = split == 1;
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, int waves, hipStream_t st, int* nparts, bool* finalized) {
+  if (!c.i8o_ok || !c.d_Uoff || !c.d_nullsum || !c.d_B8 || !c.d_i8o_tabs) return hipErrorInvalidValue;
+  switch (c.fspad / 16) {
+#define NEMO_I8O(NRV)                                                                          \
+  case NRV:                                                                                    \
+    if (c.i8o_diag && !c.i8o_nodiag)                                                           \
+      return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+                        : launch_i8o_t<NRV, 4, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
+    return waves == 8 ? launch_i8o_t<NRV, 8, false>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+                      : launch_i8o_t<NRV, 4, false>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized);
+    NEMO_I8O(1)
+    NEMO_I8O(2)
+    NEMO_I8O(4)
+#undef NEMO_I8O
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// staging for score_i8o_kernel (after d_U64, e^lo / e^hi and the int8 scale):
+// U' = U - U[S] ((fspad + 1) rows, zero past S), sum_e U[S][e] per 8-tile set
+// (left fold), and the range checks that make the offset exp safe.
+hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
+                     const std::vector<uint64_t>& d1) {
+  c.i8o_ok = false;
+  c.i8o_diag = false;
+  for (void** p : {(void**)&c.d_Uoff, (void**)&c.d_nullsum, (void**)&c.d_udig, (void**)&c.d_u0})
+    if (*p) {
+      hipFree(*p);
+      *p = nullptr;
+    }
+  const int S = c.S, E = c.E, SPAD = c.fspad;
+  if (!c.d_B8 || SPAD > 64 || SPAD < S) return hipSuccess;
+  hipError_t err = hipStreamSynchronize(c.stream);
+  if (err != hipSuccess) return err;
+  std::vector<double> U((size_t)(S + 1) * E);
+  if ((err = hipMemcpy(U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
+  const double* un = U.data() + (size_t)S * E;
+  std::vector<double> uo((size_t)(SPAD + 1) * E + 16, 0.0);
+  double umin = 0.0, umax = 0.0;
+  for (int i = 0; i < S; ++i)
+    for (int e = 0; e < E; ++e) {
+      const double v = U[(size_t)i * E + e] - un[e];
+      uo[(size_t)i * E + e] = v;
+      umin = std::min(umin, v);
+      umax = std::max(umax, v);
+    }
+  // each parent's log factor lies between 0 and its table value (lo_j or hi_j)
+  double fmin = 0.0, fmax = 0.0, gabs = 0.0;
+  for (int j = 0; j < S; ++j) {
+    const double lo = log(elo[j]), hi = log(ehi[j]);
+    fmin += std::min(0.0, std::min(lo, hi));
+    fmax += std::max(0.0, std::max(lo, hi));
+    gabs += fabs(lo);
+  }
+  // |g0| must leave the int32 room of T_0 = (acc0 << 12) + acc1 (|acc| < 2^19)
+  const double glim = 0.9 * (ldexp(1.0, 30) - ldexp(1.0, 20)) * ldexp(1.0, c.i8_cexp - 24);
+  const double padg = -std::min(500.0, glim);
+  const bool ok = std::isfinite(umin) && std::isfinite(umax) && umin + fmin >= -690.0 &&
+                  umax + fmax <= 690.0 && gabs <= glim && padg <= -40.0;
+  if (!ok) return hipSuccess;
+  const int ntiles = (E + 15) / 16, nsets = (ntiles + 7) / 8;
+  std::vector<double> ns(nsets, 0.0);
+  for (int s = 0; s < nsets; ++s) {
+    double acc = 0.0;
+    for (int e = 128 * s; e < std::min(E, 128 * s + 128); ++e) acc += un[e];
+    ns[s] = acc;
+  }
+  if (!c.d_i8o_tabs) {
+    // exp_acc's table (2^(j/2048), high dword adjusted) then log_fast's, as
+    // fill_log_table computes it; long double for correctly rounded entries
+    std::vector<uint32_t> tb(kExpTabN * 2 + 128 * 4);
+    for (int j = 0; j < kExpTabN; ++j) {
+      const double v = (double)exp2l((long double)j / kExpTabN);
+      uint64_t b;
+      memcpy(&b, &v, 8);
+      tb[2 * j] = (uint32_t)b;
+      tb[2 * j + 1] = ((uint32_t)(b >> 32) & 0x800fffffu) - ((uint32_t)j << 9);
+    }
+    double* lt = (double*)(tb.data() + kExpTabN * 2);
+    for (int k = 0; k < 128; ++k) {
+      const double inv = 1.0 / (1.0 + ((double)k + 0.5) * (1.0 / 128.0));
+      lt[2 * k] = inv;
+      lt[2 * k + 1] = (double)-logl((long double)inv);
+    }
+    if ((err = hipMalloc(&c.d_i8o_tabs, tb.size() * 4)) != hipSuccess) return err;
+    if ((err = hipMemcpy(c.d_i8o_tabs, tb.data(), tb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return err;
+  }
+  // diagonal form: U'[i][e] = u0_i + (u1_i - u0_i) D1[i][e] (within 1e-11; every U
+  // nem.py builds: U' = D ? -A : B up to the rounding of its addition chains),
+  // then U' is the free diagonal entry of the contraction (digits of u1 - u0
+  // at A[i][i], u0 in G) and the kernel reads no U at all
+  {
+    const int nwords = (E + 63) / 64;
+    bool diag = true;
+    std::vector<double> u0(S, 0.0), du(S, 0.0);
+    const double half = ldexp(1.0, c.i8_cexp - 1) * (1.0 - 1e-9);
+    for (int i = 0; i < S && diag; ++i) {
+      double ub[2] = {0.0, 0.0};
+      bool have[2] = {false, false};
+      for (int e = 0; e < E && diag; ++e) {
+        const int bit = (int)((d1[(size_t)i * nwords + e / 64] >> (e % 64)) & 1ull);
+        const double v = uo[(size_t)i * E + e];
+        if (!have[bit]) {
+          ub[bit] = v;
+          have[bit] = true;
+        } else if (fabs(v - ub[bit]) > 1e-11) {
+          diag = false;
+        }
+      }
+      u0[i] = have[0] ? ub[0] : ub[1];
+      du[i] = have[0] && have[1] ? ub[1] - ub[0] : 0.0;
+      if (!(fabs(du[i]) < half)) diag = false;
+    }
+    if (diag) {
+      std::vector<int8_t> dig((size_t)S * 8);
+      for (int i = 0; i < S; ++i) {  // the device's digit expansion (i8_prep_passes)
+        double x = ldexp(du[i], 6 - c.i8_cexp);
+        for (int sl = 0; sl < 8; ++sl) {
+          const double qd = nearbyint(x);
+          dig[(size_t)i * 8 + sl] = (int8_t)(int)qd;
+          x = (x - qd) * 64.0;
+        }
+      }
+      if ((err = hipMalloc((void**)&c.d_udig, dig.size())) != hipSuccess) return err;
+      if ((err = hipMalloc((void**)&c.d_u0, S * 8)) != hipSuccess) return err;
+      if ((err = hipMemcpy(c.d_udig, dig.data(), dig.size(), hipMemcpyHostToDevice)) != hipSuccess) return err;
+      if ((err = hipMemcpy(c.d_u0, u0.data(), S * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+      c.i8o_diag = true;
+    }
+  }
+  if ((err = hipMalloc((void**)&c.d_Uoff, uo.size() * 8)) != hipSuccess) return err;
+  if ((err = hipMalloc((void**)&c.d_nullsum, ns.size() * 8)) != hipSuccess) return err;
+  if ((err = hipMemcpy(c.d_Uoff, uo.data(), uo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = hipMemcpy(c.d_nullsum, ns.data(), ns.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  c.i8o_padg = padg;
+  c.i8o_ok = true;
+  return hipSuccess;
+}
 
 hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                            double* d_ll, int np, int waves, hipStream_t st, int* nparts,

@@ -69,6 +69,16 @@ struct Ctx {
   // int8 matrix-core variant (S <= 64): fixed-point Delta digits
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
   uint8_t* d_B8 = nullptr;         // [ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
+  // offset log-sum-exp variant (score_i8o_kernel), staged by stage_i8o
+  bool i8o_ok = false;             // staging bounds hold: |cell - U[S]| <= 690
+  double i8o_padg = 0.0;           // G of padding rows
+  double* d_Uoff = nullptr;        // [fspad + 1][E] + 16: U - U[S], zero past row S-1
+  double* d_nullsum = nullptr;     // [nsets] sum of U[S][e] over each 8-tile set
+  void* d_i8o_tabs = nullptr;      // exp table [2048] uint2 + log table [128] double2
+  bool i8o_diag = false;           // U' = u0 + du D1 per row: folded into the contraction
+  bool i8o_nodiag = false;         // option "i8o_nodiag": keep the U' loads (testing)
+  int8_t* d_udig = nullptr;        // [S][8] digits of du_i (the diagonal A entries)
+  double* d_u0 = nullptr;          // [S] u0_i, added to G
 
   // InverseMethod pair schedule (levels), cached per batch of orders
   std::vector<int32_t> inv_pos;    // the orders the schedule was built for
@@ -133,6 +143,11 @@ int factored_partials(const Ctx& c);
 hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                            double* d_ll, int np, int waves, hipStream_t st, int* nparts,
                            bool* finalized);
+// the same with the offset log-sum-exp (c.i8o_ok), waves 4 or 8 per block
+hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, int waves, hipStream_t st, int* nparts, bool* finalized);
+hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
+                     const std::vector<uint64_t>& d1);
 
 // log(x) for finite x > 0 (normal): x = 2^k m, m in [1, 2); table entry j
 // (top 7 fraction bits) holds inv_j ~ 1/(1 + (j + 0.5)/128) and L_j =

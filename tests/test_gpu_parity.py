@@ -76,6 +76,9 @@ def test_score_synthetic_golden(name, s, e):
     pos, w01 = _golden_batch(z)
     out = eng.score(pos, w01, want_cs=True, want_ow=True)
     assert np.max(np.abs(out["ll"] - z["ll"])) <= LL_TOL
+    # ll-only calls take the int8 offset kernel (U folded into the contraction)
+    assert eng.get_option("i8o") == 2
+    assert np.max(np.abs(eng.score(pos, w01) - z["ll"])) <= LL_TOL
     assert np.max(np.abs(out["cs"] - z["cs"])) <= 1e-9
     assert np.max(np.abs(out["ow"][0] - z["ow0"])) <= 1e-11
     np.testing.assert_allclose(out["ow"].sum(axis=1), 1.0, atol=1e-12)
@@ -317,8 +320,8 @@ def test_factored_detection_rejects_generic_tables():
 @pytest.mark.parametrize("s,e", [(2, 1), (11, 184), (16, 500), (33, 17), (40, 333), (64, 2000)])
 def test_factored_kernel_variants_agree(s, e):
     """Chunked (fact_kernel=1), f64 pipelined (2: 4 waves, 3: 8 waves) and
-    int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves)
-    factored kernels against the streaming kernel and the oracle: padding rows
+    int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves,
+    7 / 8: offset log-sum-exp with 4 / 8 waves) factored kernels against the streaming kernel and the oracle: padding rows
     (S % 16 != 0), ragged last tile (E % 16 != 0), tiny E; the pipelined
     kernel's bits do not depend on the batch size."""
     m = generator.synthetic_nem(s, e, 3)
@@ -334,12 +337,17 @@ def test_factored_kernel_variants_agree(s, e):
         eng.set_option("score_path", 1)
         ref = eng.score(pos, w01, cap=cap)
         eng.set_option("score_path", 2)
-        for fk in (1, 2, 3, 4, 5, 6):
+        # nem.py's U: U - U[S] is two-valued per row, so the offset kernels
+        # fold it into the contraction (i8o 2); i8o_nodiag keeps its loads
+        assert eng.get_option("i8o") == (2 if s <= 64 else 0)
+        for fk, nodiag in ((1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (7, 1), (8, 1)):
             eng.set_option("fact_kernel", fk)
+            eng.set_option("i8o_nodiag", nodiag)
             ll = eng.score(pos, w01, cap=cap)
             assert np.max(np.abs(ll - ref)) <= 1e-9, (fk, cap)
             for c in (0, 11, 36):
                 assert eng.score(pos[c:c + 1], w01[c:c + 1], cap=cap)[0] == ll[c], (fk, cap)
+        eng.set_option("i8o_nodiag", 0)
     ll = eng.score(pos, w01)
     for c in (0, 1):
         assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-9
@@ -351,6 +359,34 @@ def test_factored_kernel_variants_agree(s, e):
         eng.set_option("score_path", 1)
         assert np.max(np.abs(a - eng.score(pos[:2], wz))) <= 1e-9
         eng.set_option("score_path", 2)
+    eng.close()
+
+
+def test_offset_kernel_with_generic_u():
+    """A U whose U - U[S] is not two-valued per row (perturbed; T keeps the
+    NEM structure) takes the offset kernel that reads U - U[S] per cell
+    (i8o 1); a U far from any bound falls back to the max-offset kernel."""
+    m = generator.synthetic_nem(40, 333, 5)
+    t = m.get_score_tensor()
+    rng = np.random.default_rng(8)
+    u = m.U + rng.uniform(-0.5, 0.5, m.U.shape)
+    eng = Engine(u, t)
+    assert eng.factored and eng.get_option("i8o") == 1
+    perms = [rng.permutation(40) for _ in range(9)]
+    pos = np.array([_pos(p) for p in perms])
+    w01 = expit(rng.uniform(-3, 3, (9, 40, 40)))
+    ll = eng.score(pos, w01)
+    eng.set_option("score_path", 1)
+    assert np.max(np.abs(ll - eng.score(pos, w01))) <= 1e-9
+    eng.close()
+    for c in (0, 4):
+        assert abs(ll[c] - no.order_score(u, t, perms[c], w01[c])) <= 1e-9
+    far = m.U.copy()
+    far[3] -= 2000.0  # exp(U - U[S]) would underflow: no offset kernel
+    eng = Engine(far, t)
+    assert eng.factored and eng.get_option("i8o") == 0
+    ll = eng.score(pos, w01)
+    assert abs(ll[0] - no.order_score(far, t, perms[0], w01[0])) <= 1e-9
     eng.close()
 
 
@@ -368,11 +404,19 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
-    # 4 and 8 waves per block (auto switches at 384) give the same bits
-    for fk in (4, 6):
+    # auto is the offset kernel; its 4 and 8 waves per block (auto switches
+    # at 384) give the same bits, and so do the max-offset kernel's
+    assert eng.get_option("i8o") == 2
+    for fk in (7, 8):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
+    eng.set_option("fact_kernel", 4)
+    other = eng.score(pos, w01)
+    assert np.max(np.abs(other - big)) <= 1e-9
+    eng.set_option("fact_kernel", 6)
+    assert np.array_equal(eng.score(pos, w01), other)
+    assert np.array_equal(eng.score(pos[:7], w01[:7]), other[:7])
     eng.set_option("fact_kernel", 0)
     eng.set_option("score_path", 1)
     assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-9
@@ -453,7 +497,7 @@ def test_stage_knockdown_equals_stage_tables(s, e, dtype, cap):
     assert np.array_equal(zero, ref.score(pos[:1], np.zeros((1, s, s)), cap=cap, want_cells=True)["cells"][0])
     if dtype == "f64":
         assert np.array_equal(zero, m.U)
-    for path, fks in ((1, (0,)), (2, (0, 1, 2, 4, 6) if s <= 64 else (0, 1))):
+    for path, fks in ((1, (0,)), (2, (0, 1, 2, 4, 6, 7) if s <= 64 else (0, 1))):
         for fk in fks:
             for eng in (ref, dev):
                 eng.set_option("score_path", path)

@@ -4,7 +4,7 @@
 # removed (bits combine).  Build the variants here (CPU container) with
 # `bash tools/ablate.sh build`, then run `bash tools/ablate.sh` on the GPU.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-VARIANTS="1 2 8 9"
+VARIANTS="${VARIANTS:-1 2 8 9}"
 if [ "$1" = build ]; then
   for v in $VARIANTS; do
     python -c "import sys; sys.path.insert(0,'nem-mcmc-optimization_amd'); from nemo import build; print(build.build(out='nem-mcmc-optimization_amd/nemo/libnemo_abl$v.so', defines=['NEMO_I8_ABLATE=$v']))"
@@ -22,6 +22,7 @@ from scipy.special import expit
 from nemo import generator
 from nemo.engine import Engine
 m = generator.config_nem("C3"); eng = Engine.for_nem(m); B = 512; eng.reserve(B)
+eng.set_option("fact_kernel", int("${FK:-0}"))
 rng = np.random.default_rng(5)
 pos = torch.from_numpy(np.array([rng.permutation(64) for _ in range(B)], dtype=np.int32)).cuda()
 w01 = torch.from_numpy(expit(rng.uniform(-3, 3, (B, 64, 64)))).cuda()

@@ -23,6 +23,7 @@ def main():
         m = generator.config_nem(cfg)
         eng = Engine.for_nem(m, dtype=dtype)
         eng.set_option("score_path", int(os.environ.get("NEMO_PROF_PATH", "0")))
+        eng.set_option("fact_kernel", int(os.environ.get("NEMO_PROF_FK", "0")))
         eng.reserve(B)
         rng = np.random.default_rng(5)
         pos = torch.from_numpy(np.array([rng.permutation(S) for _ in range(B)], dtype=np.int32)).cuda()

@@ -41,7 +41,7 @@ def main():
         for batch in (32, 128, 512):
             for group in ((1, 8) if cap == 0 else (1,)):
                 variants.append((batch, group, 1, 1))
-            for fk in (1, 2, 4, 6):             # chunked, f64 pipelined, int8 x4 / x8 waves
+            for fk in (1, 2, 4, 6, 7, 8):       # chunked, f64 pipelined, int8 x4 / x8 waves, offset int8 x4 / x8
                 variants.append((batch, 1, 1, 2 + 10 * fk))
         maxb = max(v[0] for v in variants)
         eng.reserve(maxb)
