@@ -3,11 +3,12 @@ effect NEM (BASELINE.json metric, config C3; C4 = the same per GPU at N > 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--path auto|stream|factored]
 
-A step is one batched pass of the hot path over B (pos, W) evaluations whose
-inputs are already resident in HBM, enqueued on one HIP stream through the
-C-ABI: for the default path (the staged C3 table has the NEM structure, so
-the factored kernel is selected) that is prep (Delta in order positions) +
-the fp64-MFMA score kernel with fused log-sum-exp + a fixed-order finalize.
+A step is one batched pass of the hot path over B = 2048 (pos, W)
+evaluations whose inputs are already resident in HBM, enqueued on one HIP
+stream through the C-ABI: for the default path (the staged C3 model has the
+NEM structure) that is ONE kernel, score_i8o_kernel: per evaluation the
+fixed-point digits of Delta in LDS, the int8 MFMA contraction and the fp64
+log-sum-exp, with the effect sum finalized in-kernel.
 With N > 1 (torchrun, one rank per GPU) every rank evaluates its own B
 evaluations (weak scaling, no data-path collective); the only collective is
 one RCCL all-gather of per-chain best scores at the end of the timed region
@@ -68,6 +69,16 @@ def cpu_baseline(m, seconds=10.0):
                       "loop form (reference operation order), one thread, this host"}
 
 
+def load_valu_bound(key):
+    """PMC-derived VALU utilisation of the score kernel (profiles/valu.json,
+    tools/make_valu.py): VALU-busy cycles over SIMD cycles."""
+    p = os.path.join(HERE, "profiles", "valu.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        return json.load(fh).get(key)
+
+
 def load_traffic(key):
     p = os.path.join(HERE, "profiles", "traffic.json")
     if not os.path.exists(p):
@@ -110,7 +121,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("NEMO_BENCH_BATCH", 512)))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("NEMO_BENCH_BATCH", 2048)))
     ap.add_argument("--path", default=os.environ.get("NEMO_BENCH_PATH", "auto"), choices=list(PATHS))
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -196,19 +207,25 @@ def main():
         if factored:
             fpe = algorithmic_flops_per_eval(S, E, cap)
             ach = B * fpe / (kern_ms / 1e3) / 1e12
-            i8 = S <= 64 and eng.get_option("fact_kernel") in (0, 4, 5, 6, 7)
-            kname = ("score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
+            fk = eng.get_option("fact_kernel")
+            i8o = S <= 64 and eng.get_option("i8o") > 0 and fk in (0, 7, 8)
+            i8 = S <= 64 and (i8o or fk in (4, 5, 6))
+            kname = ("score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on "
+                     "v_mfma_i32_16x16x64_i8, fp64 cells, log-sum-exp offset by the null row)" if i8o else
+                     "score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
                      "fp64 cells + fused log-sum-exp)" if i8 else
                      "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)")
+            tkey = "i8o" if i8o else ("i8" if i8 else "factored")
             roof = {"bound": "mfma", "achieved": ach, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": ach / F64_MFMA_PEAK_TF,
-                    "traffic": load_traffic(f"{args.config}:{'i8' if i8 else 'factored'}:b{B}"),
+                    "traffic": load_traffic(f"{args.config}:{tkey}:b{B}"),
                     "kernel": kname, "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
                     "note": "achieved = the algorithmic fp64 contraction Delta.D1 over the permissible "
                             "pairs (2*P*E FLOP/eval) per kernel second, priced against the dense fp64 "
-                            "MFMA peak; the int8 kernel computes it exactly in 48-bit fixed point "
-                            "(DESIGN.md 3.1b) and is limited by the fp64 VALU of the fused "
-                            "log-sum-exp epilogue ((S+1)*E exps/eval)"}
+                            "MFMA peak; the int8 kernels compute it exactly in 48-bit fixed point "
+                            "(DESIGN.md 3.1a) and are bound by the fp64 VALU of the log-sum-exp "
+                            "epilogue (S*E exps/eval), not by the matrix cores: see valu_bound",
+                    "valu_bound": load_valu_bound(f"{args.config}:{tkey}:b{B}")}
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
             ach = B * bpe / (kern_ms / 1e3) / 1e9

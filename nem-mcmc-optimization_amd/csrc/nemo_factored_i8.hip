@@ -51,6 +51,15 @@ constexpr double kPadG8 = -1.0e6;    // G of padding rows: exp underflows to 0
 // lane pattern (row = lane & 15, chunk = lane >> 4) of ds_read_b128 costs 4
 // conflict cycles per read at 64- or 80-B rows, 0 at 96 B.
 constexpr int kARow = 6;
+// The offset kernel's A rows: 4 chunks (64 B) with chunk c of row i stored at
+// chunk (c + 2 ((i >> 2) & 3)) & 3 -- every 16-lane group of the
+// A-fragment ds_read_b128 (row = lane & 15, chunk = lane >> 4) then hits 16
+// distinct 16-B bank quads, and A takes 2/3 of the 96-B rows' LDS.
+template <int ROWC>
+__device__ __forceinline__ int a_byte(int i, int j) {
+  if constexpr (ROWC == 4) return i * 64 + (((j >> 4) + 2 * ((i >> 2) & 3)) & 3) * 16 + (j & 15);
+  else return i * (16 * ROWC) + j;
+}
 
 __device__ __forceinline__ double wsum(double v) {
 #pragma unroll
@@ -101,7 +110,7 @@ struct EvalLds {
 };
 
 // perm from pos, G preset (0 / kPadG8 on padding rows), digits zeroed
-template <int SPAD, int NSL>
+template <int SPAD, int NSL, int ROWC = kARow>
 __device__ __forceinline__ void i8_init_eval(EvalLds e, const int32_t* __restrict__ pb, int S, int tid,
                                              int nthreads, double padg = kPadG8) {
   for (int j = tid; j < S; j += nthreads) {
@@ -110,7 +119,7 @@ __device__ __forceinline__ void i8_init_eval(EvalLds e, const int32_t* __restric
     e.perm[pj] = j;
   }
   for (int i = tid; i < SPAD; i += nthreads) e.G[i] = i < S ? 0.0 : padg;
-  for (int k = tid; k < NSL * SPAD * kARow; k += nthreads) e.A[k] = i32x4{0, 0, 0, 0};
+  for (int k = tid; k < NSL * SPAD * ROWC; k += nthreads) e.A[k] = i32x4{0, 0, 0, 0};
 }
 
 // Delta digits and G of one evaluation, passes [k0, k0 + KB) of this wave
@@ -121,7 +130,7 @@ __device__ __forceinline__ void i8_init_eval(EvalLds e, const int32_t* __restric
 //     lo = log(1 - w + w e^lo_j), Delta = log(1 - w + w e^hi_j) - lo
 // (nem_order_mcmc.py:83-86 per factor).  The weights of the KB passes are
 // fetched first and their G sums reduced together (independent butterflies).
-template <int SPAD, int NSL, int WAVES, int KB>
+template <int SPAD, int NSL, int WAVES, int KB, int ROWC = kARow>
 __device__ __forceinline__ void i8_prep_passes(EvalLds e, int k0, int w, int lane, int S, int cap,
                                                int cexp, const double* __restrict__ w01b,
                                                const double* __restrict__ elo_s,
@@ -166,7 +175,7 @@ __device__ __forceinline__ void i8_prep_passes(EvalLds e, int k0, int w, int lan
 #pragma unroll
       for (int sl = 0; sl < NSL; ++sl) {
         const double qd = rint(x);
-        A8[(sl * SPAD + i) * (16 * kARow) + j] = (int8_t)(int)qd;
+        A8[sl * SPAD * 16 * ROWC + a_byte<ROWC>(i, j)] = (int8_t)(int)qd;
         x = (x - qd) * 64.0;
       }
     }
@@ -180,6 +189,116 @@ __device__ __forceinline__ void i8_prep_passes(EvalLds e, int k0, int w, int lan
       ga[kk] += __shfl_xor(ga[kk], o, kWave);
       gb[kk] += __shfl_xor(gb[kk], o, kWave);
     }
+  if (lane == 0) {
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const int q = w + (k0 + kk) * WAVES;
+      if (q >= npass) continue;
+      if (packed && S - 1 - q != q) e.G[e.perm[S - 1 - q]] = gb[kk];
+      e.G[e.perm[q]] = ga[kk];
+    }
+  }
+}
+
+// --- the offset kernel's prep: the same passes, cheaper arithmetic --------
+// DPP move of a double (both dwords), dpp_ctrl CTRL over all rows / banks
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)b, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ double rowsum4(double v);
+
+// sum over the wave in every lane, all VALU: quad xor 1 and 2 (quad_perm),
+// the 8-lane and 16-lane mirrors, then the permlane swaps across rows
+__device__ __forceinline__ double wsum_dpp(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  return rowsum4(v);
+}
+
+// Delta digits of one pair in integers: x = Delta 2^(6-c) in (-32, 32),
+// h = rint(x 2^18), l = rint((x 2^18 - h) 2^24) (both |.| <= 2^23, the first
+// difference exact by fma), x = h 2^-18 + l 2^-42 + <= 2^-43; then four
+// balanced base-64 digits of each: d_k = ((v + 32 (1 + 64 + 64^2)) >> 6k & 63)
+// - 32 for k < 3 and the top one (v + ...) >> 18 (in [-32, 32]).  Slices 0-3
+// hold h's digits (most significant first), 4-7 l's: the MFMA pairs then
+// rebuild T_0 = h and T_1 = l exactly.
+template <int SPAD, int ROWC>
+__device__ __forceinline__ void i8o_digits(int8_t* A8, int i, int j, double d, int cexp) {
+  const double x = ldexp(d, 6 - cexp);
+  const double hd = rint(x * 262144.0);
+  const int h = (int)hd;
+  const int l = (int)rint(fma(x, 262144.0, -hd) * 16777216.0);
+  const int off = a_byte<ROWC>(i, j);
+  constexpr int kBias = 32 * (1 + 64 + 4096);
+  const int hb = h + kBias, lb = l + kBias;
+  constexpr int SL = SPAD * 16 * ROWC;  // bytes per slice
+  A8[0 * SL + off] = (int8_t)(hb >> 18);
+  A8[1 * SL + off] = (int8_t)(((hb >> 12) & 63) - 32);
+  A8[2 * SL + off] = (int8_t)(((hb >> 6) & 63) - 32);
+  A8[3 * SL + off] = (int8_t)((hb & 63) - 32);
+  A8[4 * SL + off] = (int8_t)(lb >> 18);
+  A8[5 * SL + off] = (int8_t)(((lb >> 12) & 63) - 32);
+  A8[6 * SL + off] = (int8_t)(((lb >> 6) & 63) - 32);
+  A8[7 * SL + off] = (int8_t)((lb & 63) - 32);
+}
+
+template <int SPAD, int WAVES, int KB, int ROWC>
+__device__ __forceinline__ void i8o_prep_passes(EvalLds e, int k0, int w, int lane, int S, int cap,
+                                                int cexp, const double* __restrict__ w01b,
+                                                const double* __restrict__ elo_s,
+                                                const double* __restrict__ ehi_s,
+                                                const double2* __restrict__ ltab) {
+  const bool packed = cap == 0 || cap >= S - 1;
+  const int npass = packed ? (S + 1) / 2 : S;
+  const int p = lane;
+  int8_t* A8 = (int8_t*)e.A;
+  int ii[KB], jj[KB];
+  double sw[KB], ga[KB], gb[KB];
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) {
+    const int q = w + (k0 + kk) * WAVES;
+    int qr = 0, pp = 0;
+    bool act = false;
+    if (q < npass) {
+      if (packed) {
+        const int q2 = S - 1 - q;
+        if (p < q) { qr = q; pp = p; act = true; }
+        else { qr = q2; pp = p - q; act = q2 != q && pp < q2; }
+      } else {
+        const int np = q < cap ? q : cap;
+        qr = q; pp = q - 1 - p; act = p < np;
+      }
+    }
+    ii[kk] = act ? e.perm[qr] : -1;
+    jj[kk] = act ? e.perm[pp] : 0;
+    sw[kk] = act ? w01b[ii[kk] * S + jj[kk]] : 0.0;
+  }
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) {
+    const int q = w + (k0 + kk) * WAVES;
+    const bool act = ii[kk] >= 0;
+    double lo = 0.0;
+    if (act && !(NEMO_I8_ABLATE & 8)) {  // (8: instrumented build, no digits)
+      const int i = ii[kk], j = jj[kk];
+      lo = log_fast(fma(sw[kk], elo_s[j] - 1.0, 1.0), ltab);
+      const double d = log_fast(fma(sw[kk], ehi_s[j] - 1.0, 1.0), ltab) - lo;
+      i8o_digits<SPAD, ROWC>(A8, i, j, d, cexp);
+    }
+    ga[kk] = (act && p < q) || !packed ? lo : 0.0;
+    gb[kk] = packed && act && p >= q ? lo : 0.0;
+  }
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) {
+    ga[kk] = wsum_dpp(ga[kk]);
+    gb[kk] = wsum_dpp(gb[kk]);
+  }
   if (lane == 0) {
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
@@ -525,7 +644,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
   ev.G = ehi_s + SPAD;                                   // [SPAD]
   int* gi = (int*)(ev.G + SPAD);                         // [2][SPAD] g0, g1
   ev.perm = gi + 2 * SPAD;                               // [SPAD]
-  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][SPAD][kARow]
+  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][SPAD][4] swizzled (a_byte)
 
   const int work = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
   const int b = work / split;
@@ -547,13 +666,13 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
       ehi_s[i] = i < S ? e_hi[i] : 1.0;
     }
   }
-  i8_init_eval<SPAD, NSL>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
+  i8_init_eval<SPAD, NSL, 4>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
   __syncthreads();
   if constexpr (DIAG) {  // U' as the free diagonal "parent" i of child i (stage_i8o)
     int8_t* A8 = (int8_t*)ev.A;
     for (int k = tid; k < S * NSL; k += blockDim.x) {
       const int i = k / NSL, sl = k - i * NSL;
-      A8[(sl * SPAD + i) * (16 * kARow) + i] = udig[k];
+      A8[sl * SPAD * 64 + a_byte<4>(i, i)] = udig[k];
     }
   }
   {
@@ -561,8 +680,8 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
     const int npass = i8_npass(S, cap);
     const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
     for (int k0 = 0; k0 < my; k0 += KB)
-      i8_prep_passes<SPAD, NSL, WAVES, KB>(ev, k0, w, lane, S, cap, cexp, w01 + (size_t)b * S * S,
-                                           elo_s, ehi_s, ltab);
+      i8o_prep_passes<SPAD, WAVES, KB, 4>(ev, k0, w, lane, S, cap, cexp, w01 + (size_t)b * S * S,
+                                          elo_s, ehi_s, ltab);
   }
   __syncthreads();
   // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c))
@@ -581,7 +700,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
 
   const i32x4* Bt = (const i32x4*)B8;
   const i32x4* Gi = (const i32x4*)gi;
-  const uint32_t a_lane = (uint32_t)(col * kARow + rg);
+  const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
   int set = s_begin + w;
   if (set < s_end) {
     double lprod = 1.0;
@@ -624,8 +743,8 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
         const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
 #pragma unroll
         for (int pr = 0; pr < NP; ++pr) {
-          const i32x4 a0 = Al[((2 * pr) * SPAD + 16 * r) * kARow];
-          const i32x4 a1 = Al[((2 * pr + 1) * SPAD + 16 * r) * kARow];
+          const i32x4 a0 = Al[((2 * pr) * SPAD + 16 * r) * 4];
+          const i32x4 a1 = Al[((2 * pr + 1) * SPAD + 16 * r) * 4];
           const i32x4 ci = pr == 1 ? c0 : (pr == 3 ? c1 : i32x4{0, 0, 0, 0});
           acc[pr] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b64, ci, 0, 0, 0);
           acc[pr] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, acc[pr], 0, 0, 0);
@@ -684,7 +803,7 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   const int slots = 256 * (NEMO_I8O_WAVES_PER_SIMD * 4 / WAVES);
   int split = (slots + batch - 1) / batch;
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
-  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)8 * SPAD * 16 * kARow;
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)8 * SPAD * 64;
   const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48);
   score_i8o_kernel<NR, WAVES, DIAG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi,
@@ -814,12 +933,19 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
     }
     if (diag) {
       std::vector<int8_t> dig((size_t)S * 8);
-      for (int i = 0; i < S; ++i) {  // the device's digit expansion (i8_prep_passes)
-        double x = ldexp(du[i], 6 - c.i8_cexp);
-        for (int sl = 0; sl < 8; ++sl) {
-          const double qd = nearbyint(x);
-          dig[(size_t)i * 8 + sl] = (int8_t)(int)qd;
-          x = (x - qd) * 64.0;
+      for (int i = 0; i < S; ++i) {  // the device's digit expansion (i8o_digits)
+        const double x = ldexp(du[i], 6 - c.i8_cexp);
+        const double hd = nearbyint(x * 262144.0);
+        const int h = (int)hd;
+        const int l = (int)nearbyint(fma(x, 262144.0, -hd) * 16777216.0);
+        const int kb = 32 * (1 + 64 + 4096);
+        const int v[2] = {h + kb, l + kb};
+        for (int u = 0; u < 2; ++u) {
+          int8_t* o = dig.data() + (size_t)i * 8 + 4 * u;
+          o[0] = (int8_t)(v[u] >> 18);
+          o[1] = (int8_t)(((v[u] >> 12) & 63) - 32);
+          o[2] = (int8_t)(((v[u] >> 6) & 63) - 32);
+          o[3] = (int8_t)((v[u] & 63) - 32);
         }
       }
       if ((err = hipMalloc((void**)&c.d_udig, dig.size())) != hipSuccess) return err;

@@ -21,7 +21,7 @@ import torch
 from scipy.special import expit
 from nemo import generator
 from nemo.engine import Engine
-m = generator.config_nem("C3"); eng = Engine.for_nem(m); B = 512; eng.reserve(B)
+m = generator.config_nem("C3"); eng = Engine.for_nem(m); B = int("${ABL_B:-512}"); eng.reserve(B)
 eng.set_option("fact_kernel", int("${FK:-0}"))
 rng = np.random.default_rng(5)
 pos = torch.from_numpy(np.array([rng.permutation(64) for _ in range(B)], dtype=np.int32)).cuda()
@@ -32,6 +32,6 @@ for _ in range(5): eng.score_dev(B, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(
 torch.cuda.synchronize(); eng.timing(True)
 for _ in range(20): eng.score_dev(B, pos.data_ptr(), w01.data_ptr(), ll.data_ptr(), stream=st)
 torch.cuda.synchronize(); ms, n = eng.timing_read()
-print(f"ablate=$v kernel {ms / n * 1e3:.1f} us per 512 evals")
+print(f"ablate=$v kernel {ms / n * 1e3:.1f} us per {B} evals")
 PY
 done

@@ -1,0 +1,45 @@
+"""Turn a rocprofv3 PMC pass (SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_MFMA
+GRBM_GUI_ACTIVE SQ_WAVES) over bench.py into profiles/valu.json: how busy the
+VALU of the score kernel is.
+
+    python tools/make_valu.py <pmc_csv> <key_prefix> [profiles/valu.json]
+
+Units (MI355X_MICROARCH.md, PMC notes): SQ_ACTIVE_INST_VALU counts quad-cycles
+summed over waves; GRBM_GUI_ACTIVE is the kernel's GPU-busy cycles summed over
+the 8 XCDs.  valu_busy = 4 * SQ_ACTIVE_INST_VALU / (1024 SIMDs * GRBM_GUI_ACTIVE / 8):
+the fraction of SIMD cycles in which a VALU instruction issued.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+TAGS = (("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+        ("score_factored_kernel", "factored"), ("score_kernel", "stream"))
+
+
+def main():
+    src, prefix = sys.argv[1:3]
+    out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "valu.json")
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(src)):
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        for tag, kind in TAGS:
+            if tag in name:
+                agg[kind][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                break
+    data = json.load(open(out)) if os.path.exists(out) else {}
+    for kind, d in agg.items():
+        m = {k: sum(v) / len(v) for k, v in d.items()}
+        rec = {k: m[k] for k in sorted(m)}
+        if "SQ_ACTIVE_INST_VALU" in m and "GRBM_GUI_ACTIVE" in m:
+            rec["valu_busy"] = 4.0 * m["SQ_ACTIVE_INST_VALU"] / (1024.0 * m["GRBM_GUI_ACTIVE"] / 8.0)
+        rec["formula"] = "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)"
+        data[prefix.replace("{kind}", kind)] = rec
+    json.dump(data, open(out, "w"), indent=1)
+    print(json.dumps(data, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--configs", default="C3,C5")
+    ap.add_argument("--batches", default="32,128,512")
+    ap.add_argument("--fks", default="1,2,4,6,7,8")
     ap.add_argument("--out", default=os.path.join(HERE, "gpurun_out", "sweep.json"))
     args = ap.parse_args()
     import torch
@@ -38,10 +40,10 @@ def main():
         eng = Engine.for_nem(m, dtype=dtype)
         # (batch, group, xcd_remap, path): path 1 = stream, 2 + 10 * fact_kernel = factored
         variants = []
-        for batch in (32, 128, 512):
+        for batch in [int(v) for v in args.batches.split(",")]:
             for group in ((1, 8) if cap == 0 else (1,)):
                 variants.append((batch, group, 1, 1))
-            for fk in (1, 2, 4, 6, 7, 8):       # chunked, f64 pipelined, int8 x4 / x8 waves, offset int8 x4 / x8
+            for fk in [int(v) for v in args.fks.split(",")]:  # 1 chunked, 2 f64 pipelined, 4/6 int8 x4/x8 waves, 7/8 offset int8 x4/x8
                 variants.append((batch, 1, 1, 2 + 10 * fk))
         maxb = max(v[0] for v in variants)
         eng.reserve(maxb)
