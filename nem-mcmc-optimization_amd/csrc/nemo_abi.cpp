@@ -541,7 +541,14 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, 
   HIPCHK(hipMemcpyAsync(d_c, cvec, n * E * 8, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(d_a, anc, n * 8, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(d_x, x0, n * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(nemo::launch_local_opt_generic(c, n, d_c, d_a, d_x, d_o, st));
+  // the product form needs each factor 1 + c e (e in (0, 1)) in [1e-30, 1e30]
+  double cmin = 0.0, cmax = 0.0;
+  for (size_t k = 0; k < (size_t)n * E; ++k) {
+    cmin = std::min(cmin, cvec[k]);
+    cmax = std::max(cmax, cvec[k]);
+  }
+  const bool prod = c.local_prod && 1.0 + cmin >= 1e-30 && 1.0 + cmax <= 1e30;
+  HIPCHK(nemo::launch_local_opt_generic(c, n, d_c, d_a, d_x, d_o, prod, st));
   std::vector<double> o((size_t)n * 3);
   HIPCHK(hipMemcpyAsync(o.data(), d_o, n * 3 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipFreeAsync(d_c, st));
@@ -872,6 +879,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }
+  if (strcmp(name, "local_prod") == 0) {
+    ctx->c.local_prod = value != 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "i8o_nodiag") == 0) {
     ctx->c.i8o_nodiag = value != 0;
     return NEMO_OK;
@@ -895,6 +906,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
   else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
   else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
+  else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;
 }

@@ -26,6 +26,7 @@ struct Ctx {
   bool staged = false;
   int xcd_remap = 1;               // option "xcd_remap": XCD-aware block order
   double table_absmax = 0.0;       // max |T| over off-diagonal rows
+  bool local_prod = true;          // option "local_prod": local optima sum logs as one log of a product
   void* d_eT = nullptr;            // exp(T) [S][S][E] (dtype)
   void* d_U = nullptr;             // U [S+1][E] (dtype)
 
@@ -127,8 +128,10 @@ hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t
                                   const int32_t* d_rows, const double* d_w01, const double* d_anc,
                                   const double* d_ow, double sig0, double sig1, double* d_wnew,
                                   double* d_wdag, int32_t* d_info, hipStream_t st);
+// prod: the objective as one log of a product per lane (every factor 1 + c e,
+// e in (0, 1), within [1e-30, 1e30]; the caller checks)
 hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
-                                    const double* d_x0, double* d_out, hipStream_t st);
+                                    const double* d_x0, double* d_out, bool prod, hipStream_t st);
 
 // number of (child, parent) pairs per chain for a given cap
 int pairs_per_chain(int S, int cap);

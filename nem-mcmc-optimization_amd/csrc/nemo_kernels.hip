@@ -391,7 +391,13 @@ __device__ __forceinline__ double local_c(double lv, double owk, double s) {
   return a / b;
 }
 
-template <int NPL>
+// PROD: sum_e log(c_e e + 1) as the log of a product -- per lane, the
+// factors multiplied with a frexp renormalisation every 8 (the caller
+// guarantees 8 factors stay in range: |T| <= 40 makes each factor lie in
+// [e^-80, e^80]) and ONE log per lane, instead of a log per element.  Every
+// factor is > 0 for weights in [0, 1] (1 + e a / b = (b + e a) / b with b =
+// 1 + s (lv - 1)(1 - ow) > 0), as the reference's log needs too.
+template <int NPL, bool PROD>
 struct LocalObjective {
   double c[NPL];  // this lane's share of the c vector, kept in registers
   double anc;
@@ -401,10 +407,31 @@ struct LocalObjective {
     const double e0 = expit_d(x0);
     const double e1 = expit_d(x1);
     double p0 = 0.0, p1 = 0.0;
+    if constexpr (PROD) {
+      constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;
+      constexpr double kLn2Lo = 5.4956039718945254e-14;
+      double m0 = 1.0, m1 = 1.0;
+      int k0 = 0, k1 = 0;
 #pragma unroll
-    for (int q = 0; q < NPL; ++q) {
-      p0 += log_fast(c[q] * e0 + 1.0, ltab);
-      p1 += log_fast(c[q] * e1 + 1.0, ltab);
+      for (int q = 0; q < NPL; q += 8) {
+#pragma unroll
+        for (int u = 0; u < 8 && q + u < NPL; ++u) {  // NPL may be 4
+          m0 *= c[q + u] * e0 + 1.0;
+          m1 *= c[q + u] * e1 + 1.0;
+        }
+        k0 += __builtin_amdgcn_frexp_exp(m0);
+        m0 = __builtin_amdgcn_frexp_mant(m0);
+        k1 += __builtin_amdgcn_frexp_exp(m1);
+        m1 = __builtin_amdgcn_frexp_mant(m1);
+      }
+      p0 = fma((double)k0, kLn2Hi, log_fast(m0, ltab)) + (double)k0 * kLn2Lo;
+      p1 = fma((double)k1, kLn2Hi, log_fast(m1, ltab)) + (double)k1 * kLn2Lo;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        p0 += log_fast(c[q] * e0 + 1.0, ltab);
+        p1 += log_fast(c[q] * e1 + 1.0, ltab);
+      }
     }
     p0 = wave_sum(p0);
     p1 = wave_sum(p1);
@@ -428,7 +455,7 @@ __device__ __forceinline__ int32_t pack_info(const LbfgsResult& r) {
 constexpr int kLocalOptWavesPerSimd = NEMO_LOCAL_OPT_WAVES;
 
 // pairs of the fused per-step scorer.  grid covers nchains * npairs waves.
-template <typename TT, int NPL>
+template <typename TT, int NPL, bool PROD>
 __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_kernel(
     int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
     const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
@@ -451,7 +478,7 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
   const double s = w01[idx];
   const TT* tv = eT + ((size_t)i * S + k) * E;
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
-  LocalObjective<NPL> obj;
+  LocalObjective<NPL, PROD> obj;
   obj.ltab = ltab;
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
@@ -469,7 +496,7 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
 }
 
 // generic batch of problems with caller-given c vectors
-template <int NPL>
+template <int NPL, bool PROD>
 __global__ __launch_bounds__(256) void local_opt_generic_kernel(
     int n, int E, const double* __restrict__ cvec, const double* __restrict__ anc,
     const double* __restrict__ x0, double* __restrict__ out) {
@@ -479,7 +506,7 @@ __global__ __launch_bounds__(256) void local_opt_generic_kernel(
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (gw >= n) return;
-  LocalObjective<NPL> obj;
+  LocalObjective<NPL, PROD> obj;
   obj.ltab = ltab;
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
@@ -651,10 +678,15 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
   const size_t waves = (size_t)nchains * npairs;
   const int blocks = (int)((waves + 3) / 4);
   const TT* eT = (const TT*)c.d_eT;
-#define NEMO_LP(NPL)                                                                          \
-  local_opt_pairs_kernel<TT, NPL><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT,      \
-                                                          d_pairs, d_rows, d_w01, d_anc, d_ow, \
-                                                          sig0, sig1, d_wnew, d_wdag, d_info)
+  // the product form needs every 8 factors in range (LocalObjective)
+  const bool prod = c.local_prod && c.table_absmax <= 40.0;
+#define NEMO_LP(NPL)                                                                            \
+  if (prod)                                                                                     \
+    local_opt_pairs_kernel<TT, NPL, true><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, \
+        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);              \
+  else                                                                                          \
+    local_opt_pairs_kernel<TT, NPL, false><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, \
+        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info)
   switch (npl_for(c.E)) {
     case 4: NEMO_LP(4); break;
     case 8: NEMO_LP(8); break;
@@ -682,11 +714,12 @@ hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t
 }
 
 hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
-                                    const double* d_x0, double* d_out, hipStream_t st) {
+                                    const double* d_x0, double* d_out, bool prod, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const int blocks = (n + 3) / 4;
-#define NEMO_LG(NPL) \
-  local_opt_generic_kernel<NPL><<<blocks, 256, 0, st>>>(n, c.E, d_c, d_anc, d_x0, d_out)
+#define NEMO_LG(NPL)                                                                               \
+  if (prod) local_opt_generic_kernel<NPL, true><<<blocks, 256, 0, st>>>(n, c.E, d_c, d_anc, d_x0, d_out); \
+  else local_opt_generic_kernel<NPL, false><<<blocks, 256, 0, st>>>(n, c.E, d_c, d_anc, d_x0, d_out)
   switch (npl_for(c.E)) {
     case 4: NEMO_LG(4); break;
     case 8: NEMO_LG(8); break;

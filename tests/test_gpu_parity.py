@@ -157,10 +157,14 @@ def test_lse_kernel_matches_numpy():
 
 
 @pytest.mark.parametrize("name", ["net2_200", "C2_20"])
-def test_local_opt_vs_scipy_records(name):
+@pytest.mark.parametrize("prod", [1, 0])
+def test_local_opt_vs_scipy_records(name, prod):
+    """prod 1: the objective's sum of logs as one log of a product per lane
+    (the default); 0: a log per element."""
     z = golden(f"localopt_{name}.npz")
     e = z["c"].shape[1]
     eng = Engine(np.zeros((3, e)), np.zeros((2, 2, e)))
+    eng.set_option("local_prod", prod)
     xs, fs, nit, nfev, st = eng.local_opt(z["c"], z["anc"], z["x0"])
     assert np.all(st <= 1)
     same = (nit == z["nit"]) & (nfev == z["nfev"])
