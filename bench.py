@@ -202,6 +202,24 @@ def main():
             "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
             "includes": "H2D of pos/W/anc, eval#1 with order weights, 2016 L-BFGS-B local optima "
                         "per chain, eval#2 on binarised weights, D2H"}
+        # the whole sampler: 16 chains' host state machines (reference call order,
+        # Python random) + one fused device call per step
+        from nemo import utils as nutils
+        from nemo.chains import ChainBatch
+        order0 = nutils.initial_order_guess(m.observed_knockdown_mat)
+        seeds = [1234 + c for c in range(nch)]
+        ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue").run(2)
+        cb = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue")
+        n_it = 20
+        t0 = time.perf_counter()
+        cb.run(n_it)
+        dt = time.perf_counter() - t0
+        extras["mcmc_end_to_end"] = {
+            "chains": nch, "steps": n_it, "ms_per_step": 1e3 * dt / n_it,
+            "chain_steps_per_s": nch * n_it / dt,
+            "includes": "ChainBatch.run: proposals, reset quirks, ancestor_x (scipy inv) and "
+                        "accept per chain on the host + the fused device step",
+            "reference_cpu_s_per_chain_step": 1.2}
 
     if rank == 0:
         if factored:

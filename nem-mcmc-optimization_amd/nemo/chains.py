@@ -28,10 +28,12 @@ def shard(n_chains: int, rank: int, world: int) -> range:
     return range(start, start + base + (1 if rank < extra else 0))
 
 
-def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0):
+def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True):
     """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
     chain in ONE fused device call; each chain's state is updated exactly as
-    its own call would (same kernels, batch-invariant bits)."""
+    its own call would (same kernels, batch-invariant bits).  A failed local
+    optimisation raises the reference's Exception (nem_order_mcmc.py:168-169);
+    with ``raise_on_fail=False`` the step keeps the optimiser's last point."""
     s = chains[0].num_s
     pos = np.stack([c._pos for c in chains]).astype(np.int32)
     w = np.stack([c.parent_weights for c in chains])
@@ -42,7 +44,8 @@ def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0):
         c.ll = 0.0
         c.ancestor_x = np.clip(inv(eye - c.expit_parent_weights(w[k])) - eye, 0, 1)
         anc[k] = c.ancestor_x
-    w_new, ll1, lld, _ = engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
+    w_new, ll1, lld, _ = engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap,
+                                                raise_on_fail=raise_on_fail)
     out = np.empty(len(chains))
     for k, c in enumerate(chains):
         c._eval1 = (pos[k].copy(), w01[k].copy())
@@ -68,7 +71,8 @@ def opt_weights_batch(chains, engine: Engine, cap=0):
     return np.asarray(ll, dtype=np.float64)
 
 
-def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0):
+def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0,
+                raise_on_fail=True):
     """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
     lock-step: each MCMC step is one ``optimal_weights_batch`` call.  Chain k
     draws from ``chains[k].rng`` in the reference's call order, and ends with
@@ -77,7 +81,7 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     per-chain best scores."""
     n = len(chains)
     s = chains[0].num_s
-    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap)
+    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail)
     curr = list(opt_weights_batch(chains, engine, cap=cap))
     st = []
     for k, c in enumerate(chains):
@@ -92,7 +96,7 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
             perm, i1, i2 = c.get_new_order(st[k]["curr_perm"], swap_prob=swap_prob)
             c.reset(perm_order=perm, i1=i1, i2=i2)
             props.append(perm)
-        lls = optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap)
+        lls = optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail)
         for k, c in enumerate(chains):
             q = st[k]
             ll = float(lls[k])
@@ -127,10 +131,16 @@ class ChainBatch:
     Chain ``c`` uses ``random.Random(seed + c)`` for its proposals and
     acceptances, in exactly the reference's call order, so chain ``c`` of a
     batch reproduces a single ``NEMOrderMCMC.method`` run driven by that
-    stream."""
+    stream.  ``on_fail="raise"`` (the reference's behaviour) raises when a
+    local optimisation terminates abnormally -- at C3 most chains hit one
+    within a few dozen steps, in the reference as here; ``"continue"`` keeps
+    the optimiser's last point and goes on (an extension for long runs)."""
 
     def __init__(self, nem, init_orders, seeds, engine: Engine | None = None, gamma=None,
-                 swap_prob=0.95, use_nem=False, cap=0):
+                 swap_prob=0.95, use_nem=False, cap=0, on_fail="raise"):
+        if on_fail not in ("raise", "continue"):
+            raise ValueError(f"on_fail={on_fail!r}: 'raise' or 'continue'")
+        self.raise_on_fail = on_fail == "raise"
         self.nem = nem
         self.engine = engine if engine is not None else Engine.for_nem(nem)
         self.n = len(init_orders)
@@ -151,7 +161,8 @@ class ChainBatch:
         (nem_order_mcmc.py:257-310) for ``n_iterations`` steps.  Returns
         (best scores [n], best orders [n, S])."""
         self.best_scores = run_methods(self.chains, self.gammas, n_iterations, self.engine,
-                                       swap_prob=self.swap_prob, use_nem=self.use_nem, cap=self.cap)
+                                       swap_prob=self.swap_prob, use_nem=self.use_nem, cap=self.cap,
+                                       raise_on_fail=self.raise_on_fail)
         self.best_orders = [np.asarray(c.best_order).copy() for c in self.chains]
         self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(n_iterations, self.n)
         return self.best_scores, np.stack(self.best_orders)
