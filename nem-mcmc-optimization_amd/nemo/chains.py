@@ -28,28 +28,63 @@ def shard(n_chains: int, rank: int, world: int) -> range:
     return range(start, start + base + (1 if rank < extra else 0))
 
 
-def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True):
-    """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
-    chain in ONE fused device call; each chain's state is updated exactly as
-    its own call would (same kernels, batch-invariant bits).  A failed local
-    optimisation raises the reference's Exception (nem_order_mcmc.py:168-169);
-    with ``raise_on_fail=False`` the step keeps the optimiser's last point."""
+_LAPACK = {}
+
+
+def inv_stack(a):
+    """``scipy.linalg.inv`` of every matrix of a stack, bit for bit: the same
+    LAPACK getrf + getri calls with scipy's lwork (scipy/linalg/_basic.py
+    inv), minus its per-call validation."""
+    n = a.shape[-1]
+    if n not in _LAPACK:
+        from scipy.linalg import get_lapack_funcs
+        from scipy.linalg.lapack import _compute_lwork
+        getrf, getri, getri_lwork = get_lapack_funcs(("getrf", "getri", "getri_lwork"), (a[0],))
+        _LAPACK[n] = (getrf, getri, int(1.01 * _compute_lwork(getri_lwork, n)))
+    getrf, getri, lwork = _LAPACK[n]
+    out = np.empty_like(a)
+    for k in range(a.shape[0]):
+        if not np.all(np.isfinite(a[k])):
+            out[k] = inv(a[k])  # scipy's own error behaviour
+            continue
+        lu, piv, info = getrf(a[k])
+        if info == 0:
+            out[k], info = getri(lu, piv, lwork=lwork, overwrite_lu=1)
+        if info != 0:
+            out[k] = inv(a[k])  # scipy raises the reference's LinAlgError
+    return out
+
+
+def _prepare(chains):
+    """Host inputs of ``get_optimal_weights`` for a group of chains: positions,
+    weights, expit(weights) and ancestor_x = clip(inv(I - W~) - I, 0, 1) with W~
+    the weights under expit on the permissible entries only
+    (nem_order_mcmc.py:98-103, :185)."""
     s = chains[0].num_s
     pos = np.stack([c._pos for c in chains]).astype(np.int32)
     w = np.stack([c.parent_weights for c in chains])
     w01 = expit(w)
-    anc = np.empty_like(w)
+    sig = np.where(np.stack([c._mask for c in chains]), w01, w)
     eye = np.identity(s)
+    anc = np.clip(inv_stack(eye - sig) - eye, 0, 1)
     for k, c in enumerate(chains):
         c.ll = 0.0
-        c.ancestor_x = np.clip(inv(eye - c.expit_parent_weights(w[k])) - eye, 0, 1)
-        anc[k] = c.ancestor_x
-    w_new, ll1, lld, _ = engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap,
-                                                raise_on_fail=raise_on_fail)
+        c.ancestor_x = anc[k]
+    return pos, w, w01, anc
+
+
+def _device_step(engine: Engine, prep, cap, raise_on_fail):
+    pos, w, w01, anc = prep
+    return engine.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap, raise_on_fail=raise_on_fail)
+
+
+def _finish(chains, engine: Engine, prep, res, use_nem, cap):
+    pos, _w, w01, _anc = prep
+    w_new, ll1, lld, _ = res
     out = np.empty(len(chains))
     for k, c in enumerate(chains):
-        c._eval1 = (pos[k].copy(), w01[k].copy())
-        c.parent_weights = w_new[k].copy()
+        c._eval1 = (pos[k], w01[k])
+        c.parent_weights = w_new[k]   # a fresh array per call: the views are private
         c.ll = float(ll1[k])
         if use_nem:
             _, dag = c.create_nem(c.parent_weights)
@@ -57,6 +92,16 @@ def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on
         else:
             out[k] = float(lld[k])
     return out
+
+
+def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True):
+    """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
+    chain in ONE fused device call; each chain's state is updated exactly as
+    its own call would (same kernels, batch-invariant bits).  A failed local
+    optimisation raises the reference's Exception (nem_order_mcmc.py:168-169);
+    with ``raise_on_fail=False`` the step keeps the optimiser's last point."""
+    prep = _prepare(chains)
+    return _finish(chains, engine, prep, _device_step(engine, prep, cap, raise_on_fail), use_nem, cap)
 
 
 def opt_weights_batch(chains, engine: Engine, cap=0):
@@ -74,7 +119,7 @@ def opt_weights_batch(chains, engine: Engine, cap=0):
 def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0,
                 raise_on_fail=True):
     """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
-    lock-step: each MCMC step is one ``optimal_weights_batch`` call.  Chain k
+    lock-step: each MCMC step is one fused device call per chain group.  Chain k
     draws from ``chains[k].rng`` in the reference's call order, and ends with
     the attributes its own ``method`` call would leave (best_score, best_dag,
     best_order, score lists, parents_list of the best order).  Returns the
@@ -90,16 +135,19 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                        best_order_list=[c.perm_order], curr_dag=np.zeros((s, s)),
                        curr_list=[curr[k]], best_list=[curr[k]], all_list=[curr[k]],
                        best_parents=c.parents_list.copy(), best_struct=(c._pos, c._mask), acc=[]))
-    for _ in range(n_iterations):
-        props = []
-        for k, c in enumerate(chains):
+    props = [None] * n
+
+    def propose(idx):
+        for k in idx:
+            c = chains[k]
             perm, i1, i2 = c.get_new_order(st[k]["curr_perm"], swap_prob=swap_prob)
             c.reset(perm_order=perm, i1=i1, i2=i2)
-            props.append(perm)
-        lls = optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail)
-        for k, c in enumerate(chains):
-            q = st[k]
-            ll = float(lls[k])
+            props[k] = perm
+
+    def post(idx, lls):
+        for j, k in enumerate(idx):
+            c, q = chains[k], st[k]
+            ll = float(lls[j])
             q["all_list"].append(ll)
             dag = c.create_nem(c.parent_weights)[0] if use_nem else c.create_dag(c.parent_weights)[0]
             q["curr_list"].append(curr[k])
@@ -114,6 +162,38 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                 q["best_struct"] = (c._pos, c._mask)
                 q["best_list"].append(q["best"])
                 q["best_order_list"].append(q["best_order"])
+
+    # Two chain groups in a software pipeline: the device step of one group
+    # runs in a worker thread (ctypes releases the GIL) while the host does
+    # the other group's accept / propose / reset / ancestor_x.  Chains are
+    # independent and results are batch-invariant, so the bits are those of
+    # one batch; use_nem scores on the device in the host phase, so it runs
+    # unpipelined.
+    groups = [list(range(n))] if (use_nem or n < 2) else [list(range(n // 2)), list(range(n // 2, n))]
+    if len(groups) == 1:
+        for _ in range(n_iterations):
+            propose(groups[0])
+            post(groups[0], optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap,
+                                                  raise_on_fail=raise_on_fail))
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        pending = None
+
+        def finish(p):
+            idx, cs, prep, fut = p
+            post(idx, _finish(cs, engine, prep, fut.result(), False, cap))
+
+        with ThreadPoolExecutor(max_workers=1) as ex:
+            for _ in range(n_iterations):
+                for idx in groups:
+                    propose(idx)
+                    cs = [chains[k] for k in idx]
+                    prep = _prepare(cs)
+                    if pending is not None:
+                        finish(pending)
+                    pending = (idx, cs, prep, ex.submit(_device_step, engine, prep, cap, raise_on_fail))
+            if pending is not None:
+                finish(pending)
     for k, c in enumerate(chains):
         q = st[k]
         c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]

@@ -74,18 +74,15 @@ class NEMOrderMCMC:
         updates on reset: rows/columns i1, i2 zeroed; then per child i, the
         weight to i1 (else to i2) reset if that node is a permissible parent;
         else, for i in {i1, i2}, the *transposed* entries W[j][i] of its parents
-        set -- exactly as written there."""
+        set -- exactly as written there.  Every write stores ``init_value``, so
+        the reference's per-child loop is applied as whole-array assignments.
+        ``parents_list`` / ``n_parents`` are built on first access."""
         perm = np.asarray(perm_order)
         s = self.num_s
         pos = np.empty(s, dtype=np.int64)
         pos[perm] = np.arange(s)
         mask = self._permissible(pos)   # mask[i, j]: j in parents_list[i]
         w = self.parent_weights
-        parents_list = np.empty(s, dtype=object)
-        for i in range(s):
-            lo = max(0, pos[i] - self.cap) if self.cap else 0
-            parents_list[i] = perm[lo:pos[i]]
-        n_parents = np.array([len(p) for p in parents_list], dtype=int)
         if init:
             w[mask] = init_value
         else:
@@ -93,16 +90,41 @@ class NEMOrderMCMC:
             w[i2] = 0
             w[:, i1] = 0
             w[:, i2] = 0
-            for i in range(s):
-                if mask[i, i1]:
-                    w[i][i1] = init_value
-                elif mask[i, i2]:
-                    w[i][i2] = init_value
-                elif i == i1 or i == i2:
-                    w[parents_list[i], i] = init_value
-        self.parents_list, self.n_parents = parents_list, n_parents
-        self._pos = pos
-        self._mask = mask
+            to_i1 = mask[:, i1]
+            to_i2 = mask[:, i2] & ~to_i1
+            w[to_i1, i1] = init_value
+            w[to_i2, i2] = init_value
+            for i in (i1, i2):
+                if not to_i1[i] and not to_i2[i]:
+                    w[self._parents_of(perm, pos, i), i] = init_value
+        self._perm, self._pos, self._mask = perm, pos, mask
+        self._parents = None
+
+    def _parents_of(self, perm, pos, i):
+        lo = max(0, pos[i] - self.cap) if self.cap else 0
+        return perm[lo:pos[i]]
+
+    @property
+    def parents_list(self):
+        """parents_list[i] = the order prefix before i (within the cap), an
+        object array as in the reference (nem_order_mcmc.py:62-65)."""
+        if self._parents is None:
+            pl = np.empty(self.num_s, dtype=object)
+            for i in range(self.num_s):
+                pl[i] = self._parents_of(self._perm, self._pos, i)
+            self._parents = pl
+        return self._parents
+
+    @parents_list.setter
+    def parents_list(self, value):
+        self._parents = value
+
+    @property
+    def n_parents(self):
+        """nem_order_mcmc.py:65-66: the parent counts of the last
+        get_permissible_parents call (stale after ``method`` restores the best
+        order's parents_list, as in the reference)."""
+        return np.minimum(self._pos, self.cap).astype(int) if self.cap else self._pos.astype(int)
 
     def _permissible(self, pos):
         gap = pos[:, None] - pos[None, :]

@@ -154,6 +154,26 @@ def test_reset_quirks_match_oracle():
         perm = p1 if step % 2 else perm
 
 
+def test_inv_stack_bit_exact_to_scipy_inv():
+    """The batched ancestor_x inverse (nemo.chains.inv_stack) returns
+    scipy.linalg.inv's bits for every matrix, and its errors for a singular
+    or non-finite one (nem_order_mcmc.py:185)."""
+    from scipy.linalg import LinAlgError, inv
+    from nemo.chains import inv_stack
+    rng = np.random.default_rng(3)
+    for s in (2, 11, 64):
+        a = np.identity(s) - np.triu(rng.random((4, s, s)), 1) * 0.7 - np.tril(rng.random((4, s, s)), -1) * 0.01
+        out = inv_stack(a)
+        for k in range(4):
+            assert np.array_equal(out[k], inv(a[k]))
+    with pytest.raises(LinAlgError):
+        inv_stack(np.zeros((1, 3, 3)))
+    bad = np.identity(3)[None].copy()
+    bad[0, 0, 1] = np.nan
+    with pytest.raises(ValueError):
+        inv_stack(bad)
+
+
 def test_expit_parent_weights_and_dag():
     s = 5
     h = _HostOnly(s).obj
