@@ -174,8 +174,13 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                per block; 4 / 5 = int8 with 4 / 5 digit pairs; 6 = int8
  *                with 8 waves per block; 7 / 8 = int8 with the offset
  *                log-sum-exp (4 / 8 waves), which auto prefers when the
- *                staged model passes its range checks (option "i8o")
+ *                staged model passes its range checks (option "i8o");
+ *                9 = the banded lookup-table kernel for capped calls
+ *                (1 <= cap <= 6), which auto prefers for ll-only capped
+ *                calls when the model passes its checks (option "win")
  *   "factored"   (get only) 1 if the staged table is factorable
+ *   "win"        (get only) 1 if the capped lookup-table kernel is staged
+ *                (U - U[S] two-valued per row, partial sums in range)
  *   "i8o"        (get only) 0: no offset int8 kernel for this model; 1: it
  *                reads U - U[S] per cell; 2: U - U[S] is two-valued per row
  *                and rides in the contraction (no U reads)

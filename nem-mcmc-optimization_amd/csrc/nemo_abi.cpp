@@ -128,7 +128,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_u0};
+                  c.d_udig, c.d_u0, c.d_wuw, c.d_wnull};
   for (void* p : bufs)
     if (p) hipFree(p);
   for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
@@ -211,6 +211,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
   const int nwords = (int)((E + 63) / 64);
   c.factored = fact;
   c.i8o_ok = false;
+  c.win_ok = false;
   c.fspad = nemo::factored_spad(c.S);
   c.nwords = nwords;
   if (fact) {
@@ -246,6 +247,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
       HIPCHK(hipMemcpy(c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
     }
     HIPCHK(nemo::stage_i8o(c, elo, ehi, d1));
+    HIPCHK(nemo::stage_window(c, elo, ehi, d1));
   }
   // grow the factored scratch if a batch was reserved before staging
   if (c.cap_batch > 0) {
@@ -875,7 +877,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 8) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..8", value);
+    if (value < 0 || value > 9) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..9", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }
@@ -906,6 +908,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
   else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
   else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
+  else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;

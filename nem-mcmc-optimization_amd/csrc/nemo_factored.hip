@@ -521,7 +521,7 @@ int factored_partials(const Ctx& c) {
   const int nt = (c.E + 15) / 16;
   int n = ((c.E + cols - 1) / cols) * kFactWaves;
   for (int wv : {4, 8}) n = std::max(n, ((nt + kPipeTilesPerWave * wv - 1) / (kPipeTilesPerWave * wv)) * wv);
-  return n;
+  return std::max(n, (c.E + 63) / 64);  // the lookup-table kernel: one per word
 }
 
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
@@ -529,9 +529,15 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
                                  double* d_ow, hipStream_t st) {
   const int spad = c.fspad;
   const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
-  const bool i8_path = spad <= 64 && fk0 >= 4 && !d_cs && !d_cells && !d_ow && c.d_B8;
+  const bool ll_only0 = !d_cs && !d_cells && !d_ow;
+  // capped ll-only calls: the banded lookup-table kernel (fact_kernel 9; auto
+  // when staged), which derives its tables itself
+  const bool win = ll_only0 && c.win_ok && cap >= 1 && cap <= kWinMaxCap &&
+                   (c.fact_kernel == 0 || c.fact_kernel == 9);
+  if (c.fact_kernel == 9 && !win) return hipErrorInvalidValue;
+  const bool i8_path = spad <= 64 && fk0 >= 4 && fk0 <= 8 && ll_only0 && c.d_B8;
   hipError_t err = hipSuccess;
-  if (!i8_path) {  // the int8 kernel derives its Delta digits itself
+  if (!i8_path && !win) {  // the int8 kernel derives its Delta digits itself
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
@@ -550,11 +556,13 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool ll_only = !d_cs && !d_cells && !d_ow;
   const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
-  const bool i8 = spad <= 64 && fk >= 4 && ll_only && c.d_B8;
+  const bool i8 = spad <= 64 && fk >= 4 && fk <= 8 && ll_only && c.d_B8;
   int np = 0;
   bool finalized = false;
   const bool i8o = i8 && c.i8o_ok && (fk == 7 || fk == 8 || c.fact_kernel == 0);
-  if (i8o) {
+  if (win) {
+    err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized);
+  } else if (i8o) {
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block (auto: 8)
     const int waves = fk == 7 ? 4 : 8;
     err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, st, &np, &finalized);

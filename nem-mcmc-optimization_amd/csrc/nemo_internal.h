@@ -17,6 +17,8 @@ constexpr int kScoreWaves = 4;     // waves per score block (child split)
 constexpr int kTileCols = kWave;   // effects per score block
 constexpr int kFactWaves = 8;      // waves per factored-score block (16 effects each)
 constexpr int kI8MaxPairs = 5;     // digit-slice pairs of the int8 factored kernel
+constexpr int kWinMaxCap = 6;      // capped lookup-table kernel: parents per child
+constexpr int kWinMaxS = kMaxS;    // ... and S (LDS: ~356 S bytes per block)
 
 // Device state of one staged model on one GPU.
 struct Ctx {
@@ -80,6 +82,10 @@ struct Ctx {
   bool i8o_nodiag = false;         // option "i8o_nodiag": keep the U' loads (testing)
   int8_t* d_udig = nullptr;        // [S][8] digits of du_i (the diagonal A entries)
   double* d_u0 = nullptr;          // [S] u0_i, added to G
+  // capped lookup-table variant (score_window_kernel), staged by stage_window
+  bool win_ok = false;             // U - U[S] two-valued per row, partial sums in range
+  double* d_wuw = nullptr;         // [S][2] U - U[S] of row i at D1 bit 0 / 1
+  double* d_wnull = nullptr;       // [nwords] sum of U[S][e] over each 64-effect word
 
   // InverseMethod pair schedule (levels), cached per batch of orders
   std::vector<int32_t> inv_pos;    // the orders the schedule was built for
@@ -151,6 +157,12 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
                             double* d_ll, int waves, hipStream_t st, int* nparts, bool* finalized);
 hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
                      const std::vector<uint64_t>& d1);
+// capped lookup-table kernel (nemo_window.hip): ll only, 1 <= cap <= kWinMaxCap,
+// S <= kWinMaxS; one partial per 64-effect word (*nparts = nwords)
+hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                               double* d_ll, hipStream_t st, int* nparts, bool* finalized);
+hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
+                        const std::vector<uint64_t>& d1);
 
 // log(x) for finite x > 0 (normal): x = 2^k m, m in [1, 2); table entry j
 // (top 7 fraction bits) holds inv_j ~ 1/(1 + (j + 0.5)/128) and L_j =

@@ -1,0 +1,237 @@
+// nemo_window.hip -- order scores under a parent-set cap (BASELINE config C5:
+// S = 128, E = 5000, cap 6): a banded lookup-table kernel.
+//
+// With a cap, child q (in ORDER position) has parents q-1 .. q-cap only
+// (the build-defined cap: the last <= cap entries of the
+// order prefix).  For every table nem.py builds, parent j's log factor
+// log(1 - w + w e^{T[i][j][e]}) takes one of two values per (i, j), picked by
+// the bit D1[j][e], and U[i][e] - U[S][e] takes one of two values picked by
+// D1[i][e] (stage_window checks both).  So x = cell[q][e] - U[S][e] is a
+// function of 7 bits: node pi(q)'s own bit and those of the rows at
+// q-1 .. q-6, and so is exp(x).  Per evaluation the block tabulates it in LDS
+// as a product of two tables per row,
+//     A[q][m] = exp(U'(bit 0) + sum_{d=1..3} f_d(bit d))   (16 entries),
+//     B[q][m] = exp(sum_{d=4..6} f_d(bit d))                (8 entries),
+// and a lane (one effect) walks the rows in order with a shift register of
+// bits h: s += A[q][h & 15] * B[q][(h >> 4) & 7] -- two LDS reads and one FMA
+// per cell, no exp, instead of a K = S contraction of which only cap terms
+// are nonzero.  The column log-sum-exp is offset by the null row (as in
+// score_i8o_kernel): cs[e] = U[S][e] + log(1 + sum_q exp(x_q)); staging bounds
+// every partial sum of a cell by 690, so no entry overflows or is subnormal.
+//
+// Reference: compute_cell_ratios + calculate_ll, nem_order_mcmc.py:79-93;
+// utils.compute_ll, utils.py:84-94.
+#include <math.h>
+
+#include <algorithm>
+#include <cmath>
+#include <functional>
+
+#include "nemo_internal.h"
+
+namespace nemo {
+namespace {
+
+constexpr int kWinWaves = 8;
+constexpr int kWinLo = 16;             // entries over (self, parents 1..3)
+constexpr int kWinRow = kWinLo + 8;    // + entries over parents 4..6
+
+// LDS layout: [S][6] double2 factor scratch; [S][kWinRow] tables; per wave
+// the current word of every row as two dword arrays of odd stride (S | 1);
+// [S] int perm
+__host__ __device__ __forceinline__ size_t win_lds_bytes(int S, int waves) {
+  return ((size_t)12 * S + (size_t)kWinRow * S) * 8 + (size_t)waves * 8 * (S | 1) + (size_t)S * 4;
+}
+
+// block = (evaluation b, part of its 64-effect words); each wave walks whole
+// words (all S rows of 64 effects) and writes one partial per word
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * kWave) void score_window_kernel(
+    int S, int E, int nwords, int cap, int split, const int32_t* __restrict__ pos,
+    const double* __restrict__ w01, const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint64_t* __restrict__ D1w, const double* __restrict__ uw, const double* __restrict__ nullw,
+    double* __restrict__ partial, double* __restrict__ ll_out) {
+  extern __shared__ __attribute__((aligned(16))) double ldsw[];
+  const int rs = S | 1;
+  double2* fac = (double2*)ldsw;                               // [S][6] (f at lo, f at hi)
+  double* lut = ldsw + (size_t)12 * S;                         // [S][kWinRow]
+  uint32_t* rowbits = (uint32_t*)(lut + (size_t)S * kWinRow);  // [WAVES][2][rs]
+  int* perm = (int*)(rowbits + (size_t)WAVES * 2 * rs);        // [S]
+
+  const int b = blockIdx.x / split;
+  const int part = blockIdx.x - b * split;
+  const int wpb = (nwords + split - 1) / split;
+  const int wbeg = part * wpb, wend = min(nwords, wbeg + wpb);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int nt = blockDim.x;
+
+  for (int k = tid; k < S; k += nt) perm[k] = 0;
+  __syncthreads();
+  for (int i = tid; i < S; i += nt) {
+    int p = pos[(size_t)b * S + i];
+    p = p < 0 ? 0 : (p >= S ? S - 1 : p);  // malformed input must not fault (the ABI validates)
+    perm[p] = i;
+  }
+  __syncthreads();
+  // the two log factors of parent q-d of child q (0 past the cap / the order start)
+  const double* wb = w01 + (size_t)b * S * S;
+  for (int k = tid; k < 6 * S; k += nt) {
+    const int q = k / 6, d = k - 6 * q + 1;
+    double flo = 0.0, fhi = 0.0;
+    if (d <= cap && q >= d) {
+      const int i = perm[q], j = perm[q - d];
+      const double s = wb[(size_t)i * S + j];
+      flo = log(fma(s, e_lo[j] - 1.0, 1.0));
+      fhi = log(fma(s, e_hi[j] - 1.0, 1.0));
+    }
+    fac[k] = double2{flo, fhi};
+  }
+  __syncthreads();
+  for (int k = tid; k < kWinRow * S; k += nt) {
+    const int q = k / kWinRow, m = k - kWinRow * q;
+    const double2* f = fac + 6 * q;
+    double v;
+    if (m < kWinLo) {
+      v = uw[2 * perm[q] + (m & 1)];
+#pragma unroll
+      for (int d = 1; d <= 3; ++d) v += (m >> d) & 1 ? f[d - 1].y : f[d - 1].x;
+    } else {
+      const int mm = m - kWinLo;
+      v = mm & 1 ? f[3].y : f[3].x;
+      v += (mm >> 1) & 1 ? f[4].y : f[4].x;
+      v += (mm >> 2) & 1 ? f[5].y : f[5].x;
+    }
+    lut[k] = exp(v);
+  }
+  __syncthreads();
+
+  // lanes 0-31 read the low dwords of the row words, lanes 32-63 the high
+  // ones: two broadcast addresses per read, in different banks (odd stride)
+  uint32_t* mine = rowbits + (size_t)w * 2 * rs;
+  const uint32_t* half = mine + (lane >> 5) * rs;
+  const uint32_t bit = lane & 31;
+  for (int word = wbeg + w; word < wend; word += WAVES) {
+    // this word of every row, in order position; the wave reads back what it
+    // wrote (LDS operations of one wave complete in order)
+    for (int q = lane; q < S; q += kWave) {
+      const uint64_t v = D1w[(size_t)perm[q] * nwords + word];
+      mine[q] = (uint32_t)v;
+      mine[rs + q] = (uint32_t)(v >> 32);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t h = 0;
+    double s = 0.0;
+    const double* lq = lut;
+#pragma unroll 4
+    for (int q = 0; q < S; ++q, lq += kWinRow) {
+      h = (h << 1) | ((half[q] >> bit) & 1u);
+      s = fma(lq[h & 15], lq[kWinLo + ((h >> 4) & 7)], s);
+    }
+    double v = 64 * word + lane < E ? log1p(s) : 0.0;  // 1 = e^0 of the null row
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    if (lane == 0) partial[(size_t)b * nwords + word] = nullw[word] + v;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (split == 1) {
+    __syncthreads();
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nwords, nwords, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                               double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  if (!c.win_ok || cap < 1 || cap > kWinMaxCap || c.S > kWinMaxS) return hipErrorInvalidValue;
+  const int nwords = c.nwords;
+  // enough blocks to fill 256 CUs (LDS allows 3 per CU at S = 128); every
+  // word's partial is the same whatever the split, so bits do not depend on it
+  const int slots = 768;
+  int split = (slots + batch - 1) / batch;
+  split = std::max(1, std::min(split, (nwords + kWinWaves - 1) / kWinWaves));
+  score_window_kernel<kWinWaves><<<dim3(batch * split), kWinWaves * kWave, win_lds_bytes(c.S, kWinWaves), st>>>(
+      c.S, c.E, nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
+      c.d_fpartial, d_ll);
+  *nparts = nwords;
+  *finalized = split == 1;
+  return hipGetLastError();
+}
+
+// staging of score_window_kernel (after the factored form): U' = U - U[S]
+// two-valued per row, picked by the row's own D1 bit (within 1e-11, as
+// stage_i8o's diagonal form), the per-word sums of U[S] (left fold), and the
+// range check that keeps every table entry and the column sums finite and
+// normal for any order, any cap <= 6 and any weights in [0, 1]
+hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
+                        const std::vector<uint64_t>& d1) {
+  c.win_ok = false;
+  for (void** p : {(void**)&c.d_wuw, (void**)&c.d_wnull})
+    if (*p) {
+      hipFree(*p);
+      *p = nullptr;
+    }
+  const int S = c.S, E = c.E, nwords = c.nwords;
+  if (S > kWinMaxS || S < 1 || !c.d_D1w) return hipSuccess;
+  hipError_t err = hipStreamSynchronize(c.stream);
+  if (err != hipSuccess) return err;
+  std::vector<double> U((size_t)(S + 1) * E);
+  if ((err = hipMemcpy(U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
+  const double* un = U.data() + (size_t)S * E;
+  std::vector<double> uw(2 * (size_t)S, 0.0);
+  double umin = 0.0, umax = 0.0;
+  for (int i = 0; i < S; ++i) {
+    bool have[2] = {false, false};
+    for (int e = 0; e < E; ++e) {
+      const int bit = (int)((d1[(size_t)i * nwords + e / 64] >> (e % 64)) & 1ull);
+      const double v = U[(size_t)i * E + e] - un[e];
+      if (!std::isfinite(v)) return hipSuccess;
+      if (!have[bit]) {
+        uw[2 * i + bit] = v;
+        have[bit] = true;
+      } else if (fabs(v - uw[2 * i + bit]) > 1e-11) {
+        return hipSuccess;  // not two-valued: the general kernels only
+      }
+    }
+    if (!have[0]) uw[2 * i] = uw[2 * i + 1];
+    if (!have[1]) uw[2 * i + 1] = uw[2 * i];
+    umin = std::min({umin, uw[2 * i], uw[2 * i + 1]});
+    umax = std::max({umax, uw[2 * i], uw[2 * i + 1]});
+  }
+  // each parent's log factor lies between 0 and its table value; at most
+  // kWinMaxCap parents per child, so every partial sum of a cell is bounded too
+  std::vector<double> neg(S), posv(S);
+  for (int j = 0; j < S; ++j) {
+    const double lo = log(elo[j]), hi = log(ehi[j]);
+    neg[j] = std::min(0.0, std::min(lo, hi));
+    posv[j] = std::max(0.0, std::max(lo, hi));
+  }
+  std::sort(neg.begin(), neg.end());
+  std::sort(posv.begin(), posv.end(), std::greater<double>());
+  double fmin = 0.0, fmax = 0.0;
+  for (int k = 0; k < std::min(S, kWinMaxCap); ++k) {
+    fmin += neg[k];
+    fmax += posv[k];
+  }
+  if (!(std::isfinite(fmin) && std::isfinite(fmax) && umin + fmin >= -690.0 && umax + fmax <= 690.0))
+    return hipSuccess;
+  std::vector<double> nw(nwords, 0.0);
+  for (int k = 0; k < nwords; ++k) {
+    double acc = 0.0;
+    for (int e = 64 * k; e < std::min(E, 64 * k + 64); ++e) acc += un[e];
+    nw[k] = acc;
+  }
+  if ((err = hipMalloc((void**)&c.d_wuw, uw.size() * 8)) != hipSuccess) return err;
+  if ((err = hipMalloc((void**)&c.d_wnull, nw.size() * 8)) != hipSuccess) return err;
+  if ((err = hipMemcpy(c.d_wuw, uw.data(), uw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = hipMemcpy(c.d_wnull, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  c.win_ok = true;
+  return hipSuccess;
+}
+
+}  // namespace nemo
