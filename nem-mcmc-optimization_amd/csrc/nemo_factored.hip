@@ -529,6 +529,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
                                  double* d_ow, hipStream_t st) {
   const int spad = c.fspad;
   const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
+  if (cap >= c.S - 1) cap = 0;  // every predecessor is within the cap: no cap (same bits)
   const bool ll_only0 = !d_cs && !d_cells && !d_ow;
   // capped ll-only calls: the banded lookup-table kernel (fact_kernel 9; auto
   // when staged), which derives its tables itself
