@@ -116,6 +116,39 @@ def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, w
     return wall, kern_ms / max(launches, 1)
 
 
+def c5_capped(torch, dist, stream, batch=2048, steps=10):
+    """BASELINE config C5 (S=128, E=5000, parent cap 6): evals/s of the capped
+    lookup-table kernel (fact_kernel 9, what auto takes for capped calls) and
+    of the fp64 MFMA factored kernel (fact_kernel 1) on the same resident
+    inputs; kernel time per launch from the library's HIP events."""
+    from scipy.special import expit
+
+    from nemo import generator
+    from nemo.engine import Engine
+    S, E, _seed, cap, dtype = generator.CONFIGS["C5"]
+    eng = Engine.for_nem(generator.config_nem("C5"), dtype=dtype)
+    eng.reserve(batch)
+    rng = np.random.default_rng(78)
+    d_pos = torch.from_numpy(np.array([rng.permutation(S) for _ in range(batch)], dtype=np.int32)).cuda()
+    d_w01 = torch.from_numpy(expit(rng.uniform(-3, 3, (batch, S, S)))).cuda()
+    d_ll = torch.zeros(batch, dtype=torch.float64, device="cuda")
+    staged = bool(eng.get_option("win"))
+    out = {"workload": f"C5: S={S} E={E} cap={cap} {dtype} tables, {batch} evaluations per launch",
+           "lookup_table_staged": staged}
+    lls = {}
+    for name, fk in ((("lookup_table_kernel", 9),) if staged else ()) + (("f64_mfma_factored_kernel", 1),):
+        eng.set_option("fact_kernel", fk)
+        wall, kms = timed_steps(eng, torch, batch, cap, steps, 2, d_pos, d_w01, d_ll, stream, 1, dist)
+        lls[name] = d_ll.cpu().numpy()
+        out[name] = {"evals_per_s": batch * steps / wall, "kernel_avg_ms": kms,
+                     "cells_per_s": batch * S * E / (kms / 1e3)}
+    if staged:
+        out["max_abs_ll_diff"] = float(np.max(np.abs(lls["lookup_table_kernel"] -
+                                                     lls["f64_mfma_factored_kernel"])))
+    eng.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +253,10 @@ def main():
             "includes": "ChainBatch.run: proposals, reset quirks, ancestor_x (scipy inv) and "
                         "accept per chain on the host + the fused device step",
             "reference_cpu_s_per_chain_step": 1.2}
+        if args.config == "C3":
+            # BASELINE config C5 (128 x 5000, parent cap 6): the capped
+            # lookup-table kernel next to the fp64 MFMA factored kernel
+            extras["c5_capped"] = c5_capped(torch, dist, stream)
 
     if rank == 0:
         if factored:
