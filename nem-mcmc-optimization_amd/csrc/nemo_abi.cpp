@@ -43,8 +43,9 @@ int fail(int code, const char* fmt, ...) {
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
   if (*p) {
-    hipFree(*p);
+    hipError_t fe = hipFree(*p);
     *p = nullptr;
+    if (fe != hipSuccess) return fe;
   }
   if (n == 0) n = 1;
   return hipMalloc((void**)p, n * sizeof(T));
@@ -121,8 +122,9 @@ int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out)
 void nemo_ctx_destroy(nemo_ctx* ctx) {
   if (!ctx) return;
   Ctx& c = ctx->c;
-  hipSetDevice(c.device);
-  hipStreamSynchronize(c.stream);
+  // teardown is best effort: a failure here has no caller left to report to
+  (void)hipSetDevice(c.device);
+  (void)hipStreamSynchronize(c.stream);
   void* bufs[] = {c.d_eT,   c.d_U,    c.d_pos,  c.d_w01,  c.d_anc,     c.d_rows, c.d_sw,
                   c.d_cnt,  c.d_pairs, c.d_partial, c.d_ll, c.d_ll2, c.d_cs, c.d_ow,
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
@@ -130,9 +132,9 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
                   c.d_udig, c.d_u0, c.d_wuw, c.d_wnull};
   for (void* p : bufs)
-    if (p) hipFree(p);
-  for (hipEvent_t ev : c.ev_pool) hipEventDestroy(ev);
-  hipStreamDestroy(c.stream);
+    if (p) (void)hipFree(p);
+  for (hipEvent_t ev : c.ev_pool) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(c.stream);
   delete ctx;
 }
 
@@ -191,7 +193,7 @@ int alloc_tables(Ctx& c) {
   void** bufs[] = {&c.d_eT, &c.d_U, (void**)&c.d_U64};
   for (void** p : bufs)
     if (*p) {
-      hipFree(*p);
+      HIPCHK(hipFree(*p));
       *p = nullptr;
     }
   HIPCHK(hipMalloc(&c.d_eT, S * S * E * esz));
@@ -224,7 +226,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     // int8 variant (S <= 64): per-model fixed-point scale and the D1 bytes in
     // v_mfma_i32_16x16x64_i8 B-fragment order: tile t, lane l (effect
     // 16t + (l & 15), parents 16 (l >> 4) .. + 15), byte j = parent 16 (l >> 4) + j
-    if (c.d_B8) hipFree(c.d_B8);
+    if (c.d_B8) HIPCHK(hipFree(c.d_B8));
     c.d_B8 = nullptr;
     if (S <= 64) {
       double dmax = 0.0;

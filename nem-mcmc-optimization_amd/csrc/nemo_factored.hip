@@ -548,7 +548,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
-    hipEventRecord(e0, st);
+    { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }
   }
   // option fact_kernel: 0 auto (kAutoFactKernel for ll-only calls with
   // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,

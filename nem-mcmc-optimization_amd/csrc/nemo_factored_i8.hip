@@ -844,8 +844,9 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
   c.i8o_diag = false;
   for (void** p : {(void**)&c.d_Uoff, (void**)&c.d_nullsum, (void**)&c.d_udig, (void**)&c.d_u0})
     if (*p) {
-      hipFree(*p);
+      hipError_t fe = hipFree(*p);
       *p = nullptr;
+      if (fe != hipSuccess) return fe;
     }
   const int S = c.S, E = c.E, SPAD = c.fspad;
   if (!c.d_B8 || SPAD > 64 || SPAD < S) return hipSuccess;

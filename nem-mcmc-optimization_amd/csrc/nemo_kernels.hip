@@ -575,7 +575,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
   if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
-    hipEventRecord(e0, st);
+    { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }
   }
 #define NEMO_SC(TT, RN)                                                                      \
   score_kernel<TT, RN><<<grid, kScoreWaves * kWave, 0, st>>>(                                \
@@ -590,7 +590,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   if (e1) {
-    hipEventRecord(e1, st);
+    { hipError_t re = hipEventRecord(e1, st); if (re != hipSuccess) return re; }
     c.launches++;
   }
   finalize_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, nt, c.d_partial, d_ll);
@@ -644,7 +644,7 @@ hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStr
   if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
-    hipEventRecord(e0, st);
+    { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }
   }
   hipError_t err;
   switch (group) {
@@ -655,7 +655,7 @@ hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStr
   }
   if (err != hipSuccess) return err;
   if (e1) {
-    hipEventRecord(e1, st);
+    { hipError_t re = hipEventRecord(e1, st); if (re != hipSuccess) return re; }
     c.launches++;
   }
   finalize_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, c.ntiles(), c.d_partial, d_ll);

@@ -173,8 +173,9 @@ hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vecto
   c.win_ok = false;
   for (void** p : {(void**)&c.d_wuw, (void**)&c.d_wnull})
     if (*p) {
-      hipFree(*p);
+      hipError_t fe = hipFree(*p);
       *p = nullptr;
+      if (fe != hipSuccess) return fe;
     }
   const int S = c.S, E = c.E, nwords = c.nwords;
   if (S > kWinMaxS || S < 1 || !c.d_D1w) return hipSuccess;
