@@ -177,14 +177,19 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                staged model passes its range checks (option "i8o");
  *                9 = the banded lookup-table kernel for capped calls
  *                (1 <= cap <= 6), which auto prefers for ll-only capped
- *                calls when the model passes its checks (option "win")
+ *                calls when the model passes its checks (option "win");
+ *                10 / 11 = the offset kernel in log2 fixed point (8 / 4
+ *                waves), which auto prefers over 7 / 8 when staged
+ *                (option "i8l")
  *   "factored"   (get only) 1 if the staged table is factorable
  *   "win"        (get only) 1 if the capped lookup-table kernel is staged
  *                (U - U[S] two-valued per row, partial sums in range)
  *   "i8o"        (get only) 0: no offset int8 kernel for this model; 1: it
  *                reads U - U[S] per cell; 2: U - U[S] is two-valued per row
  *                and rides in the contraction (no U reads)
- *   "i8o_nodiag" 1 = keep the U reads even when 2 is available (testing) */
+ *   "i8o_nodiag" 1 = keep the U reads even when 2 is available (testing)
+ *   "i8l"        (get only) 1 if the log2 fixed-point offset kernel is staged
+ *                (i8o = 2 and |Delta|, |U - U[S]| / ln 2 within its digit range) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

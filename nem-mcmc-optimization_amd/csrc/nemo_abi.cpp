@@ -130,7 +130,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_u0, c.d_wuw, c.d_wnull};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (hipEvent_t ev : c.ev_pool) (void)hipEventDestroy(ev);
@@ -879,7 +879,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 9) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..9", value);
+    if (value < 0 || value > 11) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..11", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }
@@ -910,6 +910,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
   else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
   else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
+  else if (strcmp(name, "i8l") == 0) *value = c.i8l_ok ? 1 : 0;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);

@@ -229,12 +229,25 @@ __device__ __forceinline__ double wsum_dpp(double v) {
 // - 32 for k < 3 and the top one (v + ...) >> 18 (in [-32, 32]).  Slices 0-3
 // hold h's digits (most significant first), 4-7 l's: the MFMA pairs then
 // rebuild T_0 = h and T_1 = l exactly.
-template <int SPAD, int ROWC>
+// The log2 fixed-point variant (L2) writes the digits of v = d 2^20 / ln 2 in
+// the same layout: h = rint(v) (|h| < 2^25 - 2^17: top digit in [-128, 127]),
+// l = rint((v - h) 2^24), so T_0 counts units of 2^-20 and T_1 units of 2^-44
+// of y = x / ln 2.
+constexpr double kL2Scale = 1512775.3951951857;   // 2^20 / ln 2
+
+template <int SPAD, int ROWC, bool L2 = false>
 __device__ __forceinline__ void i8o_digits(int8_t* A8, int i, int j, double d, int cexp) {
-  const double x = ldexp(d, 6 - cexp);
-  const double hd = rint(x * 262144.0);
+  double hd, lr;
+  if constexpr (L2) {
+    hd = rint(d * kL2Scale);
+    lr = fma(d, kL2Scale, -hd);
+  } else {
+    const double x = ldexp(d, 6 - cexp);
+    hd = rint(x * 262144.0);
+    lr = fma(x, 262144.0, -hd);
+  }
   const int h = (int)hd;
-  const int l = (int)rint(fma(x, 262144.0, -hd) * 16777216.0);
+  const int l = (int)rint(lr * 16777216.0);
   const int off = a_byte<ROWC>(i, j);
   constexpr int kBias = 32 * (1 + 64 + 4096);
   const int hb = h + kBias, lb = l + kBias;
@@ -249,7 +262,7 @@ __device__ __forceinline__ void i8o_digits(int8_t* A8, int i, int j, double d, i
   A8[7 * SL + off] = (int8_t)((lb & 63) - 32);
 }
 
-template <int SPAD, int WAVES, int KB, int ROWC>
+template <int SPAD, int WAVES, int KB, int ROWC, bool L2 = false>
 __device__ __forceinline__ void i8o_prep_passes(EvalLds e, int k0, int w, int lane, int S, int cap,
                                                 int cexp, const double* __restrict__ w01b,
                                                 const double* __restrict__ elo_s,
@@ -289,7 +302,7 @@ __device__ __forceinline__ void i8o_prep_passes(EvalLds e, int k0, int w, int la
       const int i = ii[kk], j = jj[kk];
       lo = log_fast(fma(sw[kk], elo_s[j] - 1.0, 1.0), ltab);
       const double d = log_fast(fma(sw[kk], ehi_s[j] - 1.0, 1.0), ltab) - lo;
-      i8o_digits<SPAD, ROWC>(A8, i, j, d, cexp);
+      i8o_digits<SPAD, ROWC, L2>(A8, i, j, d, cexp);
     }
     ga[kk] = (act && p < q) || !packed ? lo : 0.0;
     gb[kk] = packed && act && p >= q ? lo : 0.0;
@@ -606,6 +619,41 @@ __device__ __forceinline__ double exp_acc(double x, const uint2* __restrict__ ta
   return fma(p, __builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), acc);
 }
 
+// acc + 2^y, y = (T_0 2^-20 + T_1 2^-44) - 1023, for the log2 fixed-point
+// variant: T_0 carries the exponent bias (G's C-init), so bits 20..30 of T_0
+// are the biased exponent 1023 + floor(y) and bits 9..19 the index j of
+// 2^(j/2048).  With the table's high dword stored with its exponent field
+// cleared, minus (j << 9) (exp_acc's table), (T_0 & ~511) + e.y is the high
+// dword of 2^(floor(y) + j/2048) -- one xor-add, no range reduction in f64.
+// The remainder rr = (T_0 & 511) + T_1 2^-24 (units of 2^-20; exact in f64)
+// lies in (-2^6, 2^9 + 2^6), so f = rr 2^-20 ln 2 is below 3.8e-4 and a
+// degree-3 series gives e^f within 9e-16.  Per cell: 3 integer + 2 cvt +
+// 5 f64 VALU and one LDS read, against 4 + 2 + 9 for exp_acc on an f64 cell.
+constexpr double kL2A1 = 6.610366635894254e-07;    // 2^-20 ln 2
+constexpr double kL2A2 = 2.1848473530471956e-13;   // kL2A1^2 / 2
+constexpr double kL2A3 = 4.814214015701685e-20;    // kL2A1^3 / 6
+
+__device__ __forceinline__ double exp2_fx_acc(uint32_t t0, int t1, const uint2* __restrict__ tab,
+                                              double acc) {
+  const uint32_t low = t0 & 511u;
+#if NEMO_I8_ABLATE & 64  // instrumented build: every lane reads entry 0 (no bank conflicts)
+  const uint2 e = tab[0];
+#else
+  // the table sits at LDS address 0 (the kernel's dynamic LDS starts there:
+  // no static LDS); an LDS-space pointer from the integer address avoids the
+  // base add of a generic pointer
+  (void)tab;
+  const uint64_t ev = *(const __attribute__((address_space(3))) uint64_t*)(size_t)((t0 >> 6) & 0x3ff8u);
+  const uint2 e{(uint32_t)ev, (uint32_t)(ev >> 32)};
+#endif
+  const uint32_t hi = (t0 ^ low) + e.y;
+  const double rr = fma((double)t1, 0x1p-24, (double)low);
+  double p = fma(rr, kL2A3, kL2A2);
+  p = fma(rr, p, kL2A1);
+  p = fma(rr, p, 1.0);
+  return fma(__builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), p, acc);
+}
+
 // sum over the four 16-lane rows (lanes col, col+16, col+32, col+48), in
 // every lane: v_permlane16_swap then v_permlane32_swap (both outputs kept)
 __device__ __forceinline__ double rowsum4(double v) {
@@ -623,7 +671,7 @@ __device__ __forceinline__ double rowsum4(double v) {
   return a0 + a1;
 }
 
-template <int NR, int WAVES, bool DIAG>
+template <int NR, int WAVES, bool DIAG, bool L2>
 __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8o_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, int cexp, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
@@ -680,17 +728,25 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
     const int npass = i8_npass(S, cap);
     const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
     for (int k0 = 0; k0 < my; k0 += KB)
-      i8o_prep_passes<SPAD, WAVES, KB, 4>(ev, k0, w, lane, S, cap, cexp, w01 + (size_t)b * S * S,
-                                          elo_s, ehi_s, ltab);
+      i8o_prep_passes<SPAD, WAVES, KB, 4, L2>(ev, k0, w, lane, S, cap, cexp,
+                                              w01 + (size_t)b * S * S, elo_s, ehi_s, ltab);
   }
   __syncthreads();
-  // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c))
+  // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c));
+  // L2: units 2^-20 / ln 2 and 2^-44 / ln 2, g0 biased by 1023 << 20 (the
+  // exponent bias of exp2_fx_acc)
   for (int i = tid; i < SPAD; i += blockDim.x) {
     const double g = DIAG && i < S ? ev.G[i] + u0[i] : ev.G[i];
-    const double g0 = rint(ldexp(g, 24 - cexp));
-    const double rho = fma(-g0, ldexp(1.0, cexp - 24), g);  // exact
-    gi[i] = (int)g0;
-    gi[SPAD + i] = (int)rint(ldexp(rho, 48 - cexp));
+    if constexpr (L2) {
+      const double g0 = rint(g * kL2Scale);
+      gi[i] = (int)g0 + (1023 << 20);
+      gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 16777216.0);
+    } else {
+      const double g0 = rint(ldexp(g, 24 - cexp));
+      const double rho = fma(-g0, ldexp(1.0, cexp - 24), g);  // exact
+      gi[i] = (int)g0;
+      gi[SPAD + i] = (int)rint(ldexp(rho, 48 - cexp));
+    }
   }
   const uint32_t uln8 = (uint32_t)(4 * rg * E + col) * 8u;  // byte offset of this lane's U' cells
   __syncthreads();
@@ -751,6 +807,13 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
+          if constexpr (L2) {  // T_0 wraps mod 2^32 only transiently (true value < 2^31)
+            const uint32_t ta = ((uint32_t)acc[0][g] << 12) + (uint32_t)acc[1][g];
+            const int tb = (int)(((uint32_t)acc[2][g] << 12) + (uint32_t)acc[3][g]);
+            if (g & 1) ls1 = exp2_fx_acc(ta, tb, etab_o, ls1);
+            else ls0 = exp2_fx_acc(ta, tb, etab_o, ls0);
+            continue;
+          }
           const int ta = (acc[0][g] << 12) + acc[1][g];
           const int tb = (acc[2][g] << 12) + acc[3][g];
           double x;
@@ -794,7 +857,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
   }
 }
 
-template <int NR, int WAVES, bool DIAG>
+template <int NR, int WAVES, bool DIAG, bool L2 = false>
 hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
@@ -805,10 +868,10 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)8 * SPAD * 64;
   const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48);
-  score_i8o_kernel<NR, WAVES, DIAG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+  score_i8o_kernel<NR, WAVES, DIAG, L2><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi,
-      c.d_B8, c.d_Uoff, c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB, c.d_fpartial, d_ll,
-      c.xcd_remap);
+      c.d_B8, c.d_Uoff, L2 ? c.d_udig2 : c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB,
+      c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
   return hipGetLastError();
@@ -817,11 +880,16 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
 }  // namespace
 
 hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                            double* d_ll, int waves, hipStream_t st, int* nparts, bool* finalized) {
+                            double* d_ll, int waves, bool l2, hipStream_t st, int* nparts,
+                            bool* finalized) {
   if (!c.i8o_ok || !c.d_Uoff || !c.d_nullsum || !c.d_B8 || !c.d_i8o_tabs) return hipErrorInvalidValue;
+  if (l2 && (!c.i8l_ok || !c.d_udig2)) return hipErrorInvalidValue;
   switch (c.fspad / 16) {
 #define NEMO_I8O(NRV)                                                                          \
   case NRV:                                                                                    \
+    if (l2)                                                                                    \
+      return waves == 8 ? launch_i8o_t<NRV, 8, true, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+                        : launch_i8o_t<NRV, 4, true, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                         : launch_i8o_t<NRV, 4, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
@@ -842,7 +910,9 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
                      const std::vector<uint64_t>& d1) {
   c.i8o_ok = false;
   c.i8o_diag = false;
-  for (void** p : {(void**)&c.d_Uoff, (void**)&c.d_nullsum, (void**)&c.d_udig, (void**)&c.d_u0})
+  c.i8l_ok = false;
+  for (void** p : {(void**)&c.d_Uoff, (void**)&c.d_nullsum, (void**)&c.d_udig, (void**)&c.d_u0,
+                   (void**)&c.d_udig2})
     if (*p) {
       hipError_t fe = hipFree(*p);
       *p = nullptr;
@@ -933,27 +1003,59 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       if (!(fabs(du[i]) < half)) diag = false;
     }
     if (diag) {
-      std::vector<int8_t> dig((size_t)S * 8);
-      for (int i = 0; i < S; ++i) {  // the device's digit expansion (i8o_digits)
-        const double x = ldexp(du[i], 6 - c.i8_cexp);
-        const double hd = nearbyint(x * 262144.0);
-        const int h = (int)hd;
-        const int l = (int)nearbyint(fma(x, 262144.0, -hd) * 16777216.0);
-        const int kb = 32 * (1 + 64 + 4096);
-        const int v[2] = {h + kb, l + kb};
-        for (int u = 0; u < 2; ++u) {
-          int8_t* o = dig.data() + (size_t)i * 8 + 4 * u;
-          o[0] = (int8_t)(v[u] >> 18);
-          o[1] = (int8_t)(((v[u] >> 12) & 63) - 32);
-          o[2] = (int8_t)(((v[u] >> 6) & 63) - 32);
-          o[3] = (int8_t)((v[u] & 63) - 32);
+      // the device's digit expansion (i8o_digits), natural scale and log2 scale
+      auto expand = [&](bool l2, std::vector<int8_t>& dig) {
+        dig.assign((size_t)S * 8, 0);
+        for (int i = 0; i < S; ++i) {
+          double hd, lr;
+          if (l2) {
+            hd = nearbyint(du[i] * kL2Scale);
+            lr = fma(du[i], kL2Scale, -hd);
+          } else {
+            const double x = ldexp(du[i], 6 - c.i8_cexp);
+            hd = nearbyint(x * 262144.0);
+            lr = fma(x, 262144.0, -hd);
+          }
+          const int h = (int)hd;
+          const int l = (int)nearbyint(lr * 16777216.0);
+          const int kb = 32 * (1 + 64 + 4096);
+          const int v[2] = {h + kb, l + kb};
+          for (int u = 0; u < 2; ++u) {
+            int8_t* o = dig.data() + (size_t)i * 8 + 4 * u;
+            o[0] = (int8_t)(v[u] >> 18);
+            o[1] = (int8_t)(((v[u] >> 12) & 63) - 32);
+            o[2] = (int8_t)(((v[u] >> 6) & 63) - 32);
+            o[3] = (int8_t)((v[u] & 63) - 32);
+          }
         }
-      }
+      };
+      std::vector<int8_t> dig, dig2;
+      expand(false, dig);
       if ((err = hipMalloc((void**)&c.d_udig, dig.size())) != hipSuccess) return err;
       if ((err = hipMalloc((void**)&c.d_u0, S * 8)) != hipSuccess) return err;
       if ((err = hipMemcpy(c.d_udig, dig.data(), dig.size(), hipMemcpyHostToDevice)) != hipSuccess) return err;
       if ((err = hipMemcpy(c.d_u0, u0.data(), S * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
       c.i8o_diag = true;
+      // log2 fixed point: every entry v = delta 2^20 / ln 2 needs |rint(v)| <
+      // 2^25 - 2^17 - 2^6 (top digit in [-128, 127] after the balancing bias),
+      // and T_0 = (x / ln 2 + 1023) 2^20 must stay in (0, 2^31): |x| <= 690
+      // (checked above) gives 27 < x / ln 2 + 1023 < 2019, and G + u0 rides
+      // in T_0's C-init, so |G + u0| / ln 2 + 1023 < 2047
+      constexpr double kLn2 = 0.69314718055994530942;
+      const double vmax = ldexp(1.0, 25) - ldexp(1.0, 17) - 128.0;
+      double dmax = 0.0, umax0 = 0.0;
+      for (int j = 0; j < S; ++j) dmax = std::max(dmax, fabs(log(ehi[j]) - log(elo[j])));
+      for (int i = 0; i < S; ++i) {
+        dmax = std::max(dmax, fabs(du[i]));
+        umax0 = std::max(umax0, fabs(u0[i]));
+      }
+      if (dmax * kL2Scale < vmax && (gabs + umax0) / kLn2 + 1023.0 < 2000.0 && -padg / kLn2 < 1000.0) {
+        expand(true, dig2);
+        if ((err = hipMalloc((void**)&c.d_udig2, dig2.size())) != hipSuccess) return err;
+        if ((err = hipMemcpy(c.d_udig2, dig2.data(), dig2.size(), hipMemcpyHostToDevice)) != hipSuccess)
+          return err;
+        c.i8l_ok = true;
+      }
     }
   }
   if ((err = hipMalloc((void**)&c.d_Uoff, uo.size() * 8)) != hipSuccess) return err;

@@ -57,7 +57,9 @@ struct Ctx {
   // shared by all children and two-valued (all tables nem.py builds)
   int score_path = 0;              // option "score_path": 0 auto, 1 stream, 2 factored
   int fact_kernel = 0;             // option "fact_kernel": 0 auto, 1 chunked, 2/3 f64 pipelined
-                                   // (4/8 waves), 4/5 int8 (4/5 digit pairs), 6 int8 x 8 waves
+                                   // (4/8 waves), 4/5 int8 (4/5 digit pairs), 6 int8 x 8 waves,
+                                   // 7/8 int8 offset LSE (4/8 waves), 9 capped lookup tables,
+                                   // 10/11 int8 offset LSE in log2 fixed point (8/4 waves)
   bool factored = false;
   int fspad = 0;                   // S rounded up to the MFMA row-block size
   int nwords = 0;                  // 64-bit words per D1 row
@@ -81,6 +83,11 @@ struct Ctx {
   bool i8o_diag = false;           // U' = u0 + du D1 per row: folded into the contraction
   bool i8o_nodiag = false;         // option "i8o_nodiag": keep the U' loads (testing)
   int8_t* d_udig = nullptr;        // [S][8] digits of du_i (the diagonal A entries)
+  // log2 fixed-point epilogue of the same kernel (stage_i8o): Delta, G and U'
+  // digits in units of 2^-20 / ln 2, so the contraction yields y = x / ln 2
+  // and 2^y is assembled from the integer accumulators (no f64 range reduction)
+  bool i8l_ok = false;             // diagonal form and the fixed-point ranges hold
+  int8_t* d_udig2 = nullptr;       // [S][8] digits of du_i / ln 2
   double* d_u0 = nullptr;          // [S] u0_i, added to G
   // capped lookup-table variant (score_window_kernel), staged by stage_window
   bool win_ok = false;             // U - U[S] two-valued per row, partial sums in range
@@ -152,9 +159,11 @@ int factored_partials(const Ctx& c);
 hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                            double* d_ll, int np, int waves, hipStream_t st, int* nparts,
                            bool* finalized);
-// the same with the offset log-sum-exp (c.i8o_ok), waves 4 or 8 per block
+// the same with the offset log-sum-exp (c.i8o_ok), waves 4 or 8 per block;
+// l2: the log2 fixed-point epilogue (c.i8l_ok)
 hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                            double* d_ll, int waves, hipStream_t st, int* nparts, bool* finalized);
+                            double* d_ll, int waves, bool l2, hipStream_t st, int* nparts,
+                            bool* finalized);
 hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
                      const std::vector<uint64_t>& d1);
 // capped lookup-table kernel (nemo_window.hip): ll only, 1 <= cap <= kWinMaxCap,

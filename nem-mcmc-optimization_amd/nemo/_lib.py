@@ -22,6 +22,8 @@ _PATH = os.environ.get("NEMO_LIBRARY") or os.path.join(os.path.dirname(os.path.a
 
 NEMO_F64, NEMO_F32 = 0, 1
 NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT = 0, -1, -2, -3, -5
+# per-pair L-BFGS-B status in the low 4 bits of ``info`` (include/nemo.h)
+LBFGSB_CONV_PGTOL, LBFGSB_CONV_REL, LBFGSB_ABNORMAL, LBFGSB_MAXITER = 0, 1, 2, 3
 
 _i32p = C.POINTER(C.c_int32)
 _f64p = C.POINTER(C.c_double)

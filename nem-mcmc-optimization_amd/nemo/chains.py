@@ -83,7 +83,7 @@ def _finish(chains, engine: Engine, prep, res, use_nem, cap):
     w_new, ll1, lld, _ = res
     out = np.empty(len(chains))
     for k, c in enumerate(chains):
-        c._eval1 = (pos[k], w01[k])
+        c._set_eval1(pos[k], w01[k])
         c.parent_weights = w_new[k]   # a fresh array per call: the views are private
         c.ll = float(ll1[k])
         if use_nem:
@@ -123,7 +123,9 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     draws from ``chains[k].rng`` in the reference's call order, and ends with
     the attributes its own ``method`` call would leave (best_score, best_dag,
     best_order, score lists, parents_list of the best order).  Returns the
-    per-chain best scores."""
+    per-chain best scores.  If a local optimisation fails and
+    ``raise_on_fail`` is set, the reference's Exception propagates and the
+    chains' states are unspecified afterwards (see the pipeline below)."""
     n = len(chains)
     s = chains[0].num_s
     optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail)
@@ -168,7 +170,11 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     # the other group's accept / propose / reset / ancestor_x.  Chains are
     # independent and results are batch-invariant, so the bits are those of
     # one batch; use_nem scores on the device in the host phase, so it runs
-    # unpipelined.
+    # unpipelined.  A failed local optimisation of one group surfaces when
+    # that group is finished, after the other group has already proposed its
+    # next order: with raise_on_fail the exception leaves the chains' states
+    # (orders, weights, RNG streams) unspecified -- only the results of runs
+    # that complete are defined to equal a sequential batched run.
     groups = [list(range(n))] if (use_nem or n < 2) else [list(range(n // 2)), list(range(n // 2, n))]
     if len(groups) == 1:
         for _ in range(n_iterations):
@@ -213,8 +219,9 @@ class ChainBatch:
     batch reproduces a single ``NEMOrderMCMC.method`` run driven by that
     stream.  ``on_fail="raise"`` (the reference's behaviour) raises when a
     local optimisation terminates abnormally -- at C3 most chains hit one
-    within a few dozen steps, in the reference as here; ``"continue"`` keeps
-    the optimiser's last point and goes on (an extension for long runs)."""
+    within a few dozen steps, in the reference as here; the chains' states
+    are unspecified after that exception.  ``"continue"`` keeps the
+    optimiser's last point and goes on (an extension for long runs)."""
 
     def __init__(self, nem, init_orders, seeds, engine: Engine | None = None, gamma=None,
                  swap_prob=0.95, use_nem=False, cap=0, on_fail="raise"):

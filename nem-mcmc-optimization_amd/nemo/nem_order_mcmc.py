@@ -30,6 +30,7 @@ from scipy.special import expit
 
 from . import utils
 from .engine import Engine, lse_full
+from ._lib import LBFGSB_ABNORMAL
 
 SIG0 = float(expit(0.0))   # expit of a binarised "no edge" weight
 SIG1 = float(expit(1.0))   # expit of a binarised "edge" weight
@@ -61,7 +62,8 @@ class NEMOrderMCMC:
         self.cell_ratios = self.compute_cell_ratios(self.parent_weights, self.score_tables)
         self.perm_order = perm_order
         self.I = np.identity(self.num_s)
-        self._eval1 = None
+        self._eval1 = None      # (pos, expit(W)) of the last eval #1
+        self._ow = None         # its order weights, computed on first access
 
     # -- A3 / A7: parent sets and the reset quirks ---------------------------
     def reset(self, perm_order, i1=None, i2=None, init=False):
@@ -184,9 +186,13 @@ class NEMOrderMCMC:
             w01 = expit(w)
             mapped = self.expit_parent_weights(w)
             self.ancestor_x = np.clip(inv(self.I - mapped) - self.I, 0, 1)
-            self._eval1 = (pos.copy(), w01.copy())
-            w_new, ll1, lld, _info = self.engine.optimal_weights(
-                pos[None, :], w01[None], self.ancestor_x[None], w[None], SIG0, SIG1, cap=self.cap)
+            self._set_eval1(pos.copy(), w01.copy())
+            # init=False re-optimises only the pairs that touch i1 / i2
+            # (nem_order_mcmc.py:190-194): the fused call optimises every
+            # permissible pair, so a failure raises only on a re-optimised one
+            w_new, ll1, lld, info = self.engine.optimal_weights(
+                pos[None, :], w01[None], self.ancestor_x[None], w[None], SIG0, SIG1, cap=self.cap,
+                raise_on_fail=init)
             w_new = w_new[0]
             if not init:
                 keep = np.zeros_like(self._mask)
@@ -194,6 +200,14 @@ class NEMOrderMCMC:
                     for k in self.parents_list[a]:
                         if not (i1 == k or i2 == k or a == i1 or a == i2):
                             keep[a, k] = True
+                redo = self._mask & ~keep
+                failed = redo & (info[0] != -1) & ((info[0] & 15) >= LBFGSB_ABNORMAL)
+                if failed.any():
+                    # the reference's first failing pair: child i ascending, parents in order
+                    a, k = min(zip(*np.nonzero(failed)), key=lambda ak: (ak[0], self._pos[ak[1]]))
+                    reason = ("ABNORMAL_TERMINATION_IN_LNSRCH" if (info[0][a, k] & 15) == LBFGSB_ABNORMAL
+                              else "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT")
+                    raise Exception(f"Minimization not successful, Reason: {reason}")
                 w_new[keep] = w[keep]
                 lld = None
             self.ll = float(ll1[0])
@@ -214,11 +228,27 @@ class NEMOrderMCMC:
             dag_ll = float(self.engine.score(pos[None, :], w01d[None], cap=self.cap)[0])
         return dag_ll
 
+    def _set_eval1(self, pos, w01):
+        self._eval1 = (pos, w01)
+        self._ow = None
+
     @property
     def order_weights(self):
-        """Order weights of the last eval #1 (set by get_optimal_weights in
-        the reference, nem_order_mcmc.py:182); fetched from HBM on access."""
-        return self.engine.order_weights(0)
+        """Order weights of this sampler's last eval #1 (the attribute
+        get_optimal_weights sets in the reference, nem_order_mcmc.py:182).
+        Computed from that evaluation's own (pos, expit(W)) on first access --
+        not read from the engine, which other samplers share."""
+        if self._ow is None:
+            if self._eval1 is None:
+                raise AttributeError("'NEMOrderMCMC' object has no attribute 'order_weights' "
+                                     "(set by get_optimal_weights)")
+            pos, w01 = self._eval1
+            self._ow = self.engine.score(pos[None, :], w01[None], cap=self.cap, want_ow=True)["ow"][0]
+        return self._ow
+
+    @order_weights.setter
+    def order_weights(self, value):
+        self._ow = np.asarray(value, dtype=np.float64)
 
     # -- A8 (single pair, API compatibility) ---------------------------------------
     def calculate_local_optimum(self, i, k):

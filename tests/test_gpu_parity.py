@@ -325,7 +325,8 @@ def test_factored_detection_rejects_generic_tables():
 def test_factored_kernel_variants_agree(s, e):
     """Chunked (fact_kernel=1), f64 pipelined (2: 4 waves, 3: 8 waves) and
     int8 fixed-point (4: 4 digit pairs, 5: 5 pairs, 6: 4 pairs x 8 waves,
-    7 / 8: offset log-sum-exp with 4 / 8 waves) factored kernels against the streaming kernel and the oracle: padding rows
+    7 / 8: offset log-sum-exp with 4 / 8 waves, 10 / 11: the same in log2
+    fixed point with 8 / 4 waves) factored kernels against the streaming kernel and the oracle: padding rows
     (S % 16 != 0), ragged last tile (E % 16 != 0), tiny E; the pipelined
     kernel's bits do not depend on the batch size."""
     m = generator.synthetic_nem(s, e, 3)
@@ -344,7 +345,9 @@ def test_factored_kernel_variants_agree(s, e):
         # nem.py's U: U - U[S] is two-valued per row, so the offset kernels
         # fold it into the contraction (i8o 2); i8o_nodiag keeps its loads
         assert eng.get_option("i8o") == (2 if s <= 64 else 0)
-        for fk, nodiag in ((1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (7, 1), (8, 1)):
+        assert eng.get_option("i8l") == (1 if s <= 64 else 0)
+        for fk, nodiag in ((1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (7, 1), (8, 1),
+                           (10, 0), (11, 0)):
             eng.set_option("fact_kernel", fk)
             eng.set_option("i8o_nodiag", nodiag)
             ll = eng.score(pos, w01, cap=cap)
@@ -408,13 +411,20 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
-    # auto is the offset kernel; its 4 and 8 waves per block (auto switches
-    # at 384) give the same bits, and so do the max-offset kernel's
-    assert eng.get_option("i8o") == 2
-    for fk in (7, 8):
+    # auto is the log2 fixed-point offset kernel; its 8 and 4 waves per block
+    # give the same bits, and so do the natural-scale offset kernel's (7 / 8)
+    # and the max-offset kernel's (4 / 6)
+    assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
+    for fk in (10, 11):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
+    eng.set_option("fact_kernel", 8)
+    nat = eng.score(pos, w01)
+    assert np.max(np.abs(nat - big)) <= 1e-9
+    eng.set_option("fact_kernel", 7)
+    assert np.array_equal(eng.score(pos, w01), nat)
+    assert np.array_equal(eng.score(pos[:7], w01[:7]), nat[:7])
     eng.set_option("fact_kernel", 4)
     other = eng.score(pos, w01)
     assert np.max(np.abs(other - big)) <= 1e-9
@@ -533,3 +543,61 @@ def test_stage_knockdown_rejects_bad_input():
         Engine.from_knockdown(m.observed_knockdown_mat, float("-inf"), m.B)
     with pytest.raises(RuntimeError, match="product range"):
         Engine.from_knockdown(m.observed_knockdown_mat, m.A, 30.0, dtype="f32")
+
+
+def test_order_weights_per_sampler_on_shared_engine():
+    """order_weights / calculate_local_optimum read THIS sampler's eval #1
+    (nem_order_mcmc.py:181-182, 160-170), also when other samplers share the
+    engine and after method()'s opt_weights pass-through scored on it."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(16, 500, 0)
+    t = m.get_score_tensor()
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(21)
+    pa, pb = rng.permutation(16), rng.permutation(16)
+    a = NEMOrderMCMC(m, pa, engine=eng)
+    b = NEMOrderMCMC(m, pb, engine=eng)
+    with pytest.raises(AttributeError):
+        a.order_weights
+    a.get_optimal_weights(init=True)
+    w_a, anc_a = a.parent_weights.copy(), a.ancestor_x.copy()
+    ora = no.OracleSampler(m.U, t, pa)
+    ora.optimal_weights()
+    b.get_optimal_weights(init=True)   # the engine's last fused call is b's
+    b.opt_weights()
+    assert np.max(np.abs(a.order_weights - ora.ow)) <= 1e-11
+    for i, k in ((int(pa[5]), int(pa[2])), (int(pa[15]), int(pa[0]))):
+        c = no.local_c(t[i][k], ora.ow[k], w_a[i][k])
+        res = no.local_optimum(c, anc_a[i][k], expit(w_a[i][k]))
+        got = a.calculate_local_optimum(i, k)
+        assert abs(got[0] - expit(res.x[0])) <= 1e-6
+    # method() on a shared engine leaves a usable order_weights
+    random.seed(5)
+    a.method(n_iterations=3, gamma=0.05, verbose=False)
+    pos, w01 = a._eval1
+    ref = no.calculate_ll(no.cell_ratios(m.U, t, no.parents_of(np.argsort(pos)), w01))[0]
+    assert np.max(np.abs(a.order_weights - ref)) <= 1e-11
+
+
+def test_init_false_reoptimises_only_pairs_touching_i1_i2():
+    """get_optimal_weights(init=False, i1, i2) (nem_order_mcmc.py:190-194):
+    pairs away from i1 / i2 keep their weights; the others get the same
+    optimum as a full pass."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(16, 500, 0)
+    eng = Engine.for_nem(m)
+    perm = np.random.default_rng(3).permutation(16)
+    full = NEMOrderMCMC(m, perm, engine=eng)
+    part = NEMOrderMCMC(m, perm, engine=eng)
+    w0 = full.parent_weights.copy()
+    full.get_optimal_weights(init=True)
+    i1, i2 = int(perm[3]), int(perm[9])
+    part.get_optimal_weights(init=False, i1=i1, i2=i2)
+    mask = part._mask
+    touch = np.zeros_like(mask)
+    touch[[i1, i2], :] = True
+    touch[:, [i1, i2]] = True
+    redo = mask & touch
+    assert redo.any() and (mask & ~touch).any()
+    assert np.array_equal(part.parent_weights[mask & ~touch], w0[mask & ~touch])
+    assert np.array_equal(part.parent_weights[redo], full.parent_weights[redo])
