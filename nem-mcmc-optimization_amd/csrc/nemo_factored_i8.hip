@@ -229,25 +229,12 @@ __device__ __forceinline__ double wsum_dpp(double v) {
 // - 32 for k < 3 and the top one (v + ...) >> 18 (in [-32, 32]).  Slices 0-3
 // hold h's digits (most significant first), 4-7 l's: the MFMA pairs then
 // rebuild T_0 = h and T_1 = l exactly.
-// The log2 fixed-point variant (L2) writes the digits of v = d 2^20 / ln 2 in
-// the same layout: h = rint(v) (|h| < 2^25 - 2^17: top digit in [-128, 127]),
-// l = rint((v - h) 2^24), so T_0 counts units of 2^-20 and T_1 units of 2^-44
-// of y = x / ln 2.
-constexpr double kL2Scale = 1512775.3951951857;   // 2^20 / ln 2
-
-template <int SPAD, int ROWC, bool L2 = false>
+template <int SPAD, int ROWC>
 __device__ __forceinline__ void i8o_digits(int8_t* A8, int i, int j, double d, int cexp) {
-  double hd, lr;
-  if constexpr (L2) {
-    hd = rint(d * kL2Scale);
-    lr = fma(d, kL2Scale, -hd);
-  } else {
-    const double x = ldexp(d, 6 - cexp);
-    hd = rint(x * 262144.0);
-    lr = fma(x, 262144.0, -hd);
-  }
+  const double x = ldexp(d, 6 - cexp);
+  const double hd = rint(x * 262144.0);
   const int h = (int)hd;
-  const int l = (int)rint(lr * 16777216.0);
+  const int l = (int)rint(fma(x, 262144.0, -hd) * 16777216.0);
   const int off = a_byte<ROWC>(i, j);
   constexpr int kBias = 32 * (1 + 64 + 4096);
   const int hb = h + kBias, lb = l + kBias;
@@ -260,6 +247,49 @@ __device__ __forceinline__ void i8o_digits(int8_t* A8, int i, int j, double d, i
   A8[5 * SL + off] = (int8_t)(((lb >> 12) & 63) - 32);
   A8[6 * SL + off] = (int8_t)(((lb >> 6) & 63) - 32);
   A8[7 * SL + off] = (int8_t)((lb & 63) - 32);
+}
+
+// The log2 fixed-point kernel (score_i8l_kernel) writes 7 slices of
+// v = d 2^20 / ln 2: h = rint(v) as above (|h| < 2^25 - 2^17: top digit in
+// [-128, 127]) in slices 0-3, and l = rint((v - h) 2^18) (|l| <= 2^17) as
+// three balanced base-64 digits in slices 4-6, so T_0 counts units of 2^-20
+// and T_1 units of 2^-38 of y = x / ln 2 (per-entry error <= 2^-39).
+constexpr double kL2Scale = 1512775.3951951857;   // 2^20 / ln 2
+
+template <int SPAD, int ROWC>
+__device__ __forceinline__ void i8l_digits(int8_t* A8, int i, int j, double d) {
+  const double hd = rint(d * kL2Scale);
+  const int h = (int)hd;
+  const int l = (int)rint(fma(d, kL2Scale, -hd) * 262144.0);
+  const int off = a_byte<ROWC>(i, j);
+  const int hb = h + 32 * (1 + 64 + 4096), lb = l + 32 * (1 + 64);
+  constexpr int SL = SPAD * 16 * ROWC;  // bytes per slice
+  A8[0 * SL + off] = (int8_t)(hb >> 18);
+  A8[1 * SL + off] = (int8_t)(((hb >> 12) & 63) - 32);
+  A8[2 * SL + off] = (int8_t)(((hb >> 6) & 63) - 32);
+  A8[3 * SL + off] = (int8_t)((hb & 63) - 32);
+  A8[4 * SL + off] = (int8_t)(lb >> 12);
+  A8[5 * SL + off] = (int8_t)(((lb >> 6) & 63) - 32);
+  A8[6 * SL + off] = (int8_t)((lb & 63) - 32);
+}
+
+// Pairwise lane swaps of a double (both dwords): dswap32 returns a's lanes
+// 0-31 next to b's lanes 0-31 (out_b: a's and b's lanes 32-63), dswap16 the
+// same per pair of 16-lane rows (v_permlane32_swap / v_permlane16_swap).
+// i8o_prep_passes builds its 8 G sums from them as a reduce-scatter.
+__device__ __forceinline__ double dswap32(double a, double b, double& out_b) {
+  const uint64_t x = __builtin_bit_cast(uint64_t, a), y = __builtin_bit_cast(uint64_t, b);
+  auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)y, false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(x >> 32), (uint32_t)(y >> 32), false, false);
+  out_b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+}
+__device__ __forceinline__ double dswap16(double a, double b, double& out_b) {
+  const uint64_t x = __builtin_bit_cast(uint64_t, a), y = __builtin_bit_cast(uint64_t, b);
+  auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)y, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(x >> 32), (uint32_t)(y >> 32), false, false);
+  out_b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
 }
 
 template <int SPAD, int WAVES, int KB, int ROWC, bool L2 = false>
@@ -302,23 +332,64 @@ __device__ __forceinline__ void i8o_prep_passes(EvalLds e, int k0, int w, int la
       const int i = ii[kk], j = jj[kk];
       lo = log_fast(fma(sw[kk], elo_s[j] - 1.0, 1.0), ltab);
       const double d = log_fast(fma(sw[kk], ehi_s[j] - 1.0, 1.0), ltab) - lo;
-      i8o_digits<SPAD, ROWC, L2>(A8, i, j, d, cexp);
+      if constexpr (L2) i8l_digits<SPAD, ROWC>(A8, i, j, d);
+      else i8o_digits<SPAD, ROWC>(A8, i, j, d, cexp);
     }
     ga[kk] = (act && p < q) || !packed ? lo : 0.0;
     gb[kk] = packed && act && p >= q ? lo : 0.0;
   }
-#pragma unroll
-  for (int kk = 0; kk < KB; ++kk) {
-    ga[kk] = wsum_dpp(ga[kk]);
-    gb[kk] = wsum_dpp(gb[kk]);
-  }
-  if (lane == 0) {
+  if constexpr (KB == 4) {
+    // reduce-scatter of the 8 sums: after the permlane32 step lanes 0-31
+    // hold pair sums of (ga[k], gb[k]) for k = 0, 1 and lanes 32-63 for
+    // k = 2, 3; after the permlane16 step row r (16 lanes) holds those of
+    // pass kk = (0, 2, 1, 3)[r] ... rows 0 / 1 / 2 / 3 -> kk 0 / 1 / 2 / 3
+    // with the operand order below; DPP folds each row.
+    double u0b, u1b, x0, x1, y0, y1;
+    double u0 = dswap32(ga[0], ga[2], u0b);   // lanes 0-31: ga0 halves, 32-63: ga2 halves
+    u0 += u0b;
+    double u1 = dswap32(gb[0], gb[2], u1b);
+    u1 += u1b;
+    double v0b, v1b;
+    double v0 = dswap32(ga[1], ga[3], v0b);
+    v0 += v0b;
+    double v1 = dswap32(gb[1], gb[3], v1b);
+    v1 += v1b;
+    // rows: u* hold kk 0 (rows 0, 1) / kk 2 (rows 2, 3); v* kk 1 / kk 3
+    x0 = dswap16(u0, v0, y0);   // row 0, 2: u0 rows (0|2) + (1|3);  row 1, 3: v0 ...
+    x0 += y0;
+    x1 = dswap16(u1, v1, y1);
+    x1 += y1;
+    // row 0: kk 0, row 1: kk 1, row 2: kk 2, row 3: kk 3 -- a and b sums
+    x0 += dpp_d<0xB1>(x0);
+    x1 += dpp_d<0xB1>(x1);
+    x0 += dpp_d<0x4E>(x0);
+    x1 += dpp_d<0x4E>(x1);
+    x0 += dpp_d<0x141>(x0);
+    x1 += dpp_d<0x141>(x1);
+    x0 += dpp_d<0x140>(x0);
+    x1 += dpp_d<0x140>(x1);
+    if ((lane & 15) == 0) {
+      const int kk = lane >> 4;
+      const int q = w + (k0 + kk) * WAVES;
+      if (q < npass) {
+        if (packed && S - 1 - q != q) e.G[e.perm[S - 1 - q]] = x1;
+        e.G[e.perm[q]] = x0;
+      }
+    }
+  } else {
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
-      const int q = w + (k0 + kk) * WAVES;
-      if (q >= npass) continue;
-      if (packed && S - 1 - q != q) e.G[e.perm[S - 1 - q]] = gb[kk];
-      e.G[e.perm[q]] = ga[kk];
+      ga[kk] = wsum_dpp(ga[kk]);
+      gb[kk] = wsum_dpp(gb[kk]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int kk = 0; kk < KB; ++kk) {
+        const int q = w + (k0 + kk) * WAVES;
+        if (q >= npass) continue;
+        if (packed && S - 1 - q != q) e.G[e.perm[S - 1 - q]] = gb[kk];
+        e.G[e.perm[q]] = ga[kk];
+      }
     }
   }
 }
@@ -619,39 +690,37 @@ __device__ __forceinline__ double exp_acc(double x, const uint2* __restrict__ ta
   return fma(p, __builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), acc);
 }
 
-// acc + 2^y, y = (T_0 2^-20 + T_1 2^-44) - 1023, for the log2 fixed-point
-// variant: T_0 carries the exponent bias (G's C-init), so bits 20..30 of T_0
-// are the biased exponent 1023 + floor(y) and bits 9..19 the index j of
-// 2^(j/2048).  With the table's high dword stored with its exponent field
-// cleared, minus (j << 9) (exp_acc's table), (T_0 & ~511) + e.y is the high
-// dword of 2^(floor(y) + j/2048) -- one xor-add, no range reduction in f64.
-// The remainder rr = (T_0 & 511) + T_1 2^-24 (units of 2^-20; exact in f64)
-// lies in (-2^6, 2^9 + 2^6), so f = rr 2^-20 ln 2 is below 3.8e-4 and a
-// degree-3 series gives e^f within 9e-16.  Per cell: 3 integer + 2 cvt +
-// 5 f64 VALU and one LDS read, against 4 + 2 + 9 for exp_acc on an f64 cell.
-constexpr double kL2A1 = 6.610366635894254e-07;    // 2^-20 ln 2
-constexpr double kL2A2 = 2.1848473530471956e-13;   // kL2A1^2 / 2
-constexpr double kL2A3 = 4.814214015701685e-20;    // kL2A1^3 / 6
+// acc + 2^y for score_i8l_kernel, y = (T_0 2^-20 + T_1 2^-38) - 1023: T_0
+// carries the exponent bias (G's C-init), so bits 20..30 of T_0 are the
+// biased exponent 1023 + floor(y) and bits 9..19 the index j of 2^(j/2048).
+// The table's high dword is stored with its exponent field cleared, minus
+// (j << 9) (exp_acc's table), so (T_0 & ~511) + e.y is the high dword of
+// 2^(floor(y) + j/2048): no range reduction in f64.  The remainder
+// R = (T_0 & 511) 2^18 + T_1 (units of 2^-38, |R| < 2^28: one shift-add and
+// one conversion, exact) gives f = R 2^-38 ln 2 in (-2.2e-5, 3.6e-4) and a
+// degree-3 series e^f within 8e-16.  Per cell: 5 integer + 1 cvt + 4 f64 VALU
+// and one LDS read, against 4 + 2 + 9 for exp_acc on an f64 cell.
+constexpr double kL2A1 = 2.521654753072454e-12;    // 2^-38 ln 2
+constexpr double kL2A2 = 3.1793713468464492e-24;   // kL2A1^2 / 2
+constexpr double kL2A3 = 2.672425622852573e-36;    // kL2A1^3 / 6
 
-__device__ __forceinline__ double exp2_fx_acc(uint32_t t0, int t1, const uint2* __restrict__ tab,
-                                              double acc) {
+__device__ __forceinline__ double exp2_fx_acc(uint32_t t0, int t1, double acc) {
   const uint32_t low = t0 & 511u;
 #if NEMO_I8_ABLATE & 64  // instrumented build: every lane reads entry 0 (no bank conflicts)
-  const uint2 e = tab[0];
+  const uint32_t addr = 0u;
 #else
-  // the table sits at LDS address 0 (the kernel's dynamic LDS starts there:
-  // no static LDS); an LDS-space pointer from the integer address avoids the
-  // base add of a generic pointer
-  (void)tab;
-  const uint64_t ev = *(const __attribute__((address_space(3))) uint64_t*)(size_t)((t0 >> 6) & 0x3ff8u);
-  const uint2 e{(uint32_t)ev, (uint32_t)(ev >> 32)};
+  const uint32_t addr = (t0 >> 6) & 0x3ff8u;
 #endif
-  const uint32_t hi = (t0 ^ low) + e.y;
-  const double rr = fma((double)t1, 0x1p-24, (double)low);
-  double p = fma(rr, kL2A3, kL2A2);
-  p = fma(rr, p, kL2A1);
-  p = fma(rr, p, 1.0);
-  return fma(__builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), p, acc);
+  // the table sits at LDS address 0 (the kernel's dynamic LDS starts there:
+  // it has no static LDS); an LDS-space pointer from the integer address
+  // avoids the base add of a generic pointer
+  const uint64_t ev = *(const __attribute__((address_space(3))) uint64_t*)(size_t)addr;
+  const uint32_t hi = (t0 ^ low) + (uint32_t)(ev >> 32);
+  const double r = (double)(int)((low << 18) + (uint32_t)t1);
+  double p = fma(r, kL2A3, kL2A2);
+  p = fma(r, p, kL2A1);
+  p = fma(r, p, 1.0);
+  return fma(__builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)ev), p, acc);
 }
 
 // sum over the four 16-lane rows (lanes col, col+16, col+32, col+48), in
@@ -671,7 +740,7 @@ __device__ __forceinline__ double rowsum4(double v) {
   return a0 + a1;
 }
 
-template <int NR, int WAVES, bool DIAG, bool L2>
+template <int NR, int WAVES, bool DIAG>
 __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8o_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, int cexp, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
@@ -728,25 +797,17 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
     const int npass = i8_npass(S, cap);
     const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
     for (int k0 = 0; k0 < my; k0 += KB)
-      i8o_prep_passes<SPAD, WAVES, KB, 4, L2>(ev, k0, w, lane, S, cap, cexp,
-                                              w01 + (size_t)b * S * S, elo_s, ehi_s, ltab);
+      i8o_prep_passes<SPAD, WAVES, KB, 4>(ev, k0, w, lane, S, cap, cexp, w01 + (size_t)b * S * S,
+                                          elo_s, ehi_s, ltab);
   }
   __syncthreads();
-  // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c));
-  // L2: units 2^-20 / ln 2 and 2^-44 / ln 2, g0 biased by 1023 << 20 (the
-  // exponent bias of exp2_fx_acc)
+  // G in fixed point: g0 = rint(G 2^(24-c)), g1 = rint((G - g0 2^(c-24)) 2^(48-c))
   for (int i = tid; i < SPAD; i += blockDim.x) {
     const double g = DIAG && i < S ? ev.G[i] + u0[i] : ev.G[i];
-    if constexpr (L2) {
-      const double g0 = rint(g * kL2Scale);
-      gi[i] = (int)g0 + (1023 << 20);
-      gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 16777216.0);
-    } else {
-      const double g0 = rint(ldexp(g, 24 - cexp));
-      const double rho = fma(-g0, ldexp(1.0, cexp - 24), g);  // exact
-      gi[i] = (int)g0;
-      gi[SPAD + i] = (int)rint(ldexp(rho, 48 - cexp));
-    }
+    const double g0 = rint(ldexp(g, 24 - cexp));
+    const double rho = fma(-g0, ldexp(1.0, cexp - 24), g);  // exact
+    gi[i] = (int)g0;
+    gi[SPAD + i] = (int)rint(ldexp(rho, 48 - cexp));
   }
   const uint32_t uln8 = (uint32_t)(4 * rg * E + col) * 8u;  // byte offset of this lane's U' cells
   __syncthreads();
@@ -807,13 +868,6 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
         }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          if constexpr (L2) {  // T_0 wraps mod 2^32 only transiently (true value < 2^31)
-            const uint32_t ta = ((uint32_t)acc[0][g] << 12) + (uint32_t)acc[1][g];
-            const int tb = (int)(((uint32_t)acc[2][g] << 12) + (uint32_t)acc[3][g]);
-            if (g & 1) ls1 = exp2_fx_acc(ta, tb, etab_o, ls1);
-            else ls0 = exp2_fx_acc(ta, tb, etab_o, ls0);
-            continue;
-          }
           const int ta = (acc[0][g] << 12) + acc[1][g];
           const int tb = (acc[2][g] << 12) + acc[3][g];
           double x;
@@ -857,7 +911,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
   }
 }
 
-template <int NR, int WAVES, bool DIAG, bool L2 = false>
+template <int NR, int WAVES, bool DIAG>
 hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
@@ -868,10 +922,183 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)8 * SPAD * 64;
   const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48);
-  score_i8o_kernel<NR, WAVES, DIAG, L2><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+  score_i8o_kernel<NR, WAVES, DIAG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi,
-      c.d_B8, c.d_Uoff, L2 ? c.d_udig2 : c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB,
-      c.d_fpartial, d_ll, c.xcd_remap);
+      c.d_B8, c.d_Uoff, c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB, c.d_fpartial, d_ll,
+      c.xcd_remap);
+  *nparts = nsets;
+  *finalized = split == 1;
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// score_i8l_kernel: score_i8o_kernel's contraction and offset log-sum-exp
+// with every table quantity in units of 1 / ln 2 (digits of Delta / ln 2,
+// U' / ln 2 on the diagonal, G / ln 2), so the contraction yields
+// y = x / ln 2 in fixed point and 2^y = e^x is assembled from the integer
+// accumulators (exp2_fx_acc).  T_0 = acc_0 2^12 + acc_1 (slices 0-3, units
+// 2^-20, G's high part and the exponent bias 1023 << 20 in acc_1's C-init);
+// T_1 = acc_2 2^12 + acc_3 (slice 4; slices 5-6 with G's low part as C-init,
+// units 2^-38): 7 MFMAs per row block against 8.  Requires the diagonal form
+// (stage_i8o).
+// ---------------------------------------------------------------------------
+template <int NR, int WAVES>
+__global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8l_kernel(
+    int S, int E, int ntiles, int nsets, int split, int cap, double padg,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const int8_t* __restrict__ udig, const double* __restrict__ u0,
+    const double* __restrict__ nullsum, const void* __restrict__ tabs,
+    double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
+  constexpr int SPAD = NR * 16;
+  constexpr int NSL = 7;
+  extern __shared__ __attribute__((aligned(16))) double lds8[];
+  uint2* etab_o = (uint2*)lds8;                          // [kExpTabN] at LDS address 0
+  double2* ltab = (double2*)(etab_o + kExpTabN);         // [128] log table
+  double* elo_s = (double*)(ltab + 128);                 // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  EvalLds ev;
+  ev.G = ehi_s + SPAD;                                   // [SPAD]
+  int* gi = (int*)(ev.G + SPAD);                         // [2][SPAD] g0, g1
+  ev.perm = gi + 2 * SPAD;                               // [SPAD]
+  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][SPAD][4] swizzled (a_byte)
+
+  const int work = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / split;
+  const int part = work - b * split;
+  const int spb = (nsets + split - 1) / split;
+  const int s_begin = part * spb;
+  const int s_end = min(nsets, s_begin + spb);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int col = lane & 15, rg = lane >> 4;
+
+  {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    const int4* src = (const int4*)tabs;
+    int4* dst = (int4*)lds8;
+    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+  }
+  i8_init_eval<SPAD, NSL, 4>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
+  __syncthreads();
+  {  // U' / ln 2 as the free diagonal "parent" i of child i
+    int8_t* A8 = (int8_t*)ev.A;
+    for (int k = tid; k < S * NSL; k += blockDim.x) {
+      const int i = k / NSL, sl = k - i * NSL;
+      A8[sl * SPAD * 64 + a_byte<4>(i, i)] = udig[i * 8 + sl];
+    }
+  }
+  {
+    constexpr int KB = 4;
+    const int npass = i8_npass(S, cap);
+    const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
+    for (int k0 = 0; k0 < my; k0 += KB)
+      i8o_prep_passes<SPAD, WAVES, KB, 4, true>(ev, k0, w, lane, S, cap, 0, w01 + (size_t)b * S * S,
+                                                elo_s, ehi_s, ltab);
+  }
+  __syncthreads();
+  // G + u0 in units of 2^-20 / ln 2: g0 = rint(.) + (1023 << 20) (the exponent
+  // bias of exp2_fx_acc), g1 = the remainder in units of 2^-38 / ln 2 (the
+  // C-init of slices 5-6); |g1| <= 2^17.  G is one value per row, so its
+  // rounding is systematic over the effects: it gets T_1's full resolution.
+  for (int i = tid; i < SPAD; i += blockDim.x) {
+    const double g = i < S ? ev.G[i] + u0[i] : ev.G[i];
+    const double g0 = rint(g * kL2Scale);
+    gi[i] = (int)g0 + (1023 << 20);
+    gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 262144.0);
+  }
+  __syncthreads();
+#if NEMO_I8_ABLATE & 32  // instrumented build (tools/ablate.sh): prep only, no tiles
+  if (s_end > 0) return;
+#endif
+
+  const i32x4* Bt = (const i32x4*)B8;
+  const i32x4* Gi = (const i32x4*)gi;
+  const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
+  int set = s_begin + w;
+  if (set < s_end) {
+    double lprod = 1.0;
+    int lexp = 0;
+    int t = 8 * set;
+    i32x4 bc = Bt[(size_t)t * kWave + lane];
+    for (;;) {
+      uint32_t ao = a_lane;
+      asm volatile("" : "+v"(ao));
+      const i32x4* Al = ev.A + ao;
+      int tn = t + 1, setn = set;
+      if (tn >= min(ntiles, 8 * set + 8)) {
+        setn = set + WAVES;
+        tn = 8 * setn;
+      }
+      const bool more = setn < s_end;
+      const int tl = more ? tn : t;  // prefetch target (the current tile again at the end)
+      const i32x4 b1 = bc;
+      const i32x4 b64 = b1 << 6;
+      bc = Bt[(size_t)tl * kWave + lane];
+      double ls0 = 0.0, ls1 = 0.0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+        const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+        auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
+        i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0), b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1), b1, h0, 0, 0, 0);
+        i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2), b64, c0, 0, 0, 0);
+        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3), b1, h1, 0, 0, 0);
+        const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4), b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5), b64, c1, 0, 0, 0);
+        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6), b1, l1, 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          // T_0 wraps mod 2^32 only transiently (its true value is in (0, 2^31))
+          const uint32_t t0 = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+          const int t1 = (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]);
+          if (g & 1) ls1 = exp2_fx_acc(t0, t1, ls1);
+          else ls0 = exp2_fx_acc(t0, t1, ls0);
+        }
+      }
+      double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
+      lprod *= t * 16 + col < E ? l : 1.0;
+      lexp += __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      if (setn != set) {  // set complete: one partial
+        double v = log(lprod) + (double)lexp * 0.69314718055994530942;
+        v = wsum(lane < 16 ? v : 0.0);
+        if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+        lprod = 1.0;
+        lexp = 0;
+      }
+      if (!more) break;
+      t = tn;
+      set = setn;
+    }
+  }
+  if (split == 1) {
+    __syncthreads();
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nsets, nsets, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
+}
+
+template <int NR, int WAVES>
+hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                        double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  const int nsets = (ntiles + 7) / 8;
+  const int slots = 256 * (NEMO_I8O_WAVES_PER_SIMD * 4 / WAVES);
+  int split = (slots + batch - 1) / batch;
+  split = split < 1 ? 1 : (split > nsets ? nsets : split);
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)7 * SPAD * 64;
+  score_i8l_kernel<NR, WAVES><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
   return hipGetLastError();
@@ -888,8 +1115,8 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
 #define NEMO_I8O(NRV)                                                                          \
   case NRV:                                                                                    \
     if (l2)                                                                                    \
-      return waves == 8 ? launch_i8o_t<NRV, 8, true, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
-                        : launch_i8o_t<NRV, 4, true, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
+      return waves == 8 ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+                        : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                         : launch_i8o_t<NRV, 4, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
@@ -1003,7 +1230,7 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       if (!(fabs(du[i]) < half)) diag = false;
     }
     if (diag) {
-      // the device's digit expansion (i8o_digits), natural scale and log2 scale
+      // the device's digit expansion (i8o_digits, i8l_digits)
       auto expand = [&](bool l2, std::vector<int8_t>& dig) {
         dig.assign((size_t)S * 8, 0);
         for (int i = 0; i < S; ++i) {
@@ -1017,15 +1244,24 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
             lr = fma(x, 262144.0, -hd);
           }
           const int h = (int)hd;
-          const int l = (int)nearbyint(lr * 16777216.0);
           const int kb = 32 * (1 + 64 + 4096);
-          const int v[2] = {h + kb, l + kb};
-          for (int u = 0; u < 2; ++u) {
-            int8_t* o = dig.data() + (size_t)i * 8 + 4 * u;
-            o[0] = (int8_t)(v[u] >> 18);
-            o[1] = (int8_t)(((v[u] >> 12) & 63) - 32);
-            o[2] = (int8_t)(((v[u] >> 6) & 63) - 32);
-            o[3] = (int8_t)((v[u] & 63) - 32);
+          int8_t* o = dig.data() + (size_t)i * 8;
+          const int hb = h + kb;
+          o[0] = (int8_t)(hb >> 18);
+          o[1] = (int8_t)(((hb >> 12) & 63) - 32);
+          o[2] = (int8_t)(((hb >> 6) & 63) - 32);
+          o[3] = (int8_t)((hb & 63) - 32);
+          if (l2) {  // i8l_digits: l in units of 2^-38, three digits, slice 7 unused
+            const int lb = (int)nearbyint(lr * 262144.0) + 32 * (1 + 64);
+            o[4] = (int8_t)(lb >> 12);
+            o[5] = (int8_t)(((lb >> 6) & 63) - 32);
+            o[6] = (int8_t)((lb & 63) - 32);
+          } else {
+            const int lb = (int)nearbyint(lr * 16777216.0) + kb;
+            o[4] = (int8_t)(lb >> 18);
+            o[5] = (int8_t)(((lb >> 12) & 63) - 32);
+            o[6] = (int8_t)(((lb >> 6) & 63) - 32);
+            o[7] = (int8_t)((lb & 63) - 32);
           }
         }
       };

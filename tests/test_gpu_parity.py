@@ -351,13 +351,16 @@ def test_factored_kernel_variants_agree(s, e):
             eng.set_option("fact_kernel", fk)
             eng.set_option("i8o_nodiag", nodiag)
             ll = eng.score(pos, w01, cap=cap)
-            assert np.max(np.abs(ll - ref)) <= 1e-9, (fk, cap)
+            # 10 / 11 carry the fraction of each entry to 2^-38 / ln 2 (7 slices;
+            # DESIGN.md 3.1e): ~1e-9 at 64 x 2000, the others ~1e-11
+            tol = 1e-8 if fk in (10, 11) else 1e-9
+            assert np.max(np.abs(ll - ref)) <= tol, (fk, cap)
             for c in (0, 11, 36):
                 assert eng.score(pos[c:c + 1], w01[c:c + 1], cap=cap)[0] == ll[c], (fk, cap)
         eng.set_option("i8o_nodiag", 0)
-    ll = eng.score(pos, w01)
+    ll = eng.score(pos, w01)   # fact_kernel 11 (log2 fixed point)
     for c in (0, 1):
-        assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-9
+        assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c])) <= 1e-8
     # zero and one weights (G, Delta at their extremes)
     for w in (0.0, 1.0):
         wz = np.full((2, s, s), w)
@@ -421,19 +424,19 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
     eng.set_option("fact_kernel", 8)
     nat = eng.score(pos, w01)
-    assert np.max(np.abs(nat - big)) <= 1e-9
+    assert np.max(np.abs(nat - big)) <= 1e-8
     eng.set_option("fact_kernel", 7)
     assert np.array_equal(eng.score(pos, w01), nat)
     assert np.array_equal(eng.score(pos[:7], w01[:7]), nat[:7])
     eng.set_option("fact_kernel", 4)
     other = eng.score(pos, w01)
-    assert np.max(np.abs(other - big)) <= 1e-9
+    assert np.max(np.abs(other - nat)) <= 1e-9
     eng.set_option("fact_kernel", 6)
     assert np.array_equal(eng.score(pos, w01), other)
     assert np.array_equal(eng.score(pos[:7], w01[:7]), other[:7])
     eng.set_option("fact_kernel", 0)
     eng.set_option("score_path", 1)
-    assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-9
+    assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-8
     eng.set_option("score_path", 0)
 
 

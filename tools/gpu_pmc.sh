@@ -7,7 +7,7 @@ n=0
 while read -r ctrs; do
   [ -z "$ctrs" ] && continue
   n=$((n+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$R/$OUT/p$n" -o p -- python "$R/tools/prof_target.py" --reps 2 > "$OUT/p$n.log" 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $ctrs --output-format csv -d "$R/$OUT/p$n" -o p -- python "$R/tools/prof_target.py" --reps 2 > "$OUT/p$n.log" 2>&1
   rc=$?; echo "pass $n [$ctrs] rc=$rc"
   if [ $rc -ge 124 ]; then echo "stopping"; exit $rc; fi
 done < "$1"
