@@ -704,8 +704,8 @@ constexpr double kL2A1 = 2.521654753072454e-12;    // 2^-38 ln 2
 constexpr double kL2A2 = 3.1793713468464492e-24;   // kL2A1^2 / 2
 constexpr double kL2A3 = 2.672425622852573e-36;    // kL2A1^3 / 6
 
-__device__ __forceinline__ double exp2_fx_acc(uint32_t t0, int t1, double acc) {
-  const uint32_t low = t0 & 511u;
+// split in three so a caller can keep several table reads in flight
+__device__ __forceinline__ uint64_t exp2_fx_load(uint32_t t0) {
 #if NEMO_I8_ABLATE & 64  // instrumented build: every lane reads entry 0 (no bank conflicts)
   const uint32_t addr = 0u;
 #else
@@ -714,12 +714,16 @@ __device__ __forceinline__ double exp2_fx_acc(uint32_t t0, int t1, double acc) {
   // the table sits at LDS address 0 (the kernel's dynamic LDS starts there:
   // it has no static LDS); an LDS-space pointer from the integer address
   // avoids the base add of a generic pointer
-  const uint64_t ev = *(const __attribute__((address_space(3))) uint64_t*)(size_t)addr;
-  const uint32_t hi = (t0 ^ low) + (uint32_t)(ev >> 32);
-  const double r = (double)(int)((low << 18) + (uint32_t)t1);
+  return *(const __attribute__((address_space(3))) uint64_t*)(size_t)addr;
+}
+__device__ __forceinline__ double exp2_fx_series(uint32_t t0, int t1) {
+  const double r = (double)(int)(((t0 & 511u) << 18) + (uint32_t)t1);
   double p = fma(r, kL2A3, kL2A2);
   p = fma(r, p, kL2A1);
-  p = fma(r, p, 1.0);
+  return fma(r, p, 1.0);
+}
+__device__ __forceinline__ double exp2_fx_apply(uint32_t t0, uint64_t ev, double p, double acc) {
+  const uint32_t hi = (t0 & ~511u) + (uint32_t)(ev >> 32);
   return fma(__builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)ev), p, acc);
 }
 
@@ -1044,7 +1048,15 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
       for (int r = 0; r < NR; ++r) {
         const i32x4 c0 = Gi[(16 * r) / 4 + rg];
         const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+#if NEMO_I8_ABLATE & 128  // instrumented build: half the A-fragment reads (wrong values)
+        auto A = [&](int sl) { return Al[((sl & ~1) * SPAD + 16 * r) * 4]; };
+#else
         auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
+#endif
+#if NEMO_I8_ABLATE & 2  // instrumented build: no MFMA (one add per pair; wrong values)
+        const i32x4 h0 = A(0) + A(1) + b64, h1 = A(2) + A(3) + c0, l0 = A(4) + b1,
+                    l1 = A(5) + A(6) + c1;
+#else
         i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0), b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
         h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1), b1, h0, 0, 0, 0);
         i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2), b64, c0, 0, 0, 0);
@@ -1052,13 +1064,26 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
         const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4), b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
         i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5), b64, c1, 0, 0, 0);
         l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6), b1, l1, 0, 0, 0);
+#endif
+        // the row block's 4 cells per lane in three phases, so the 4 table
+        // reads (random entries: ~3.5-way bank conflicts) are in flight
+        // while the series runs: addresses + reads, series, then assembly
+        uint32_t t0[4];
+        uint64_t ev[4];
+        double pr[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           // T_0 wraps mod 2^32 only transiently (its true value is in (0, 2^31))
-          const uint32_t t0 = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
-          const int t1 = (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]);
-          if (g & 1) ls1 = exp2_fx_acc(t0, t1, ls1);
-          else ls0 = exp2_fx_acc(t0, t1, ls0);
+          t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+          ev[g] = exp2_fx_load(t0[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (g & 1) ls1 = exp2_fx_apply(t0[g], ev[g], pr[g], ls1);
+          else ls0 = exp2_fx_apply(t0[g], ev[g], pr[g], ls0);
         }
       }
       double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row

@@ -12,7 +12,7 @@ if [ "$1" = build ]; then
   exit 0
 fi
 mkdir -p gpurun_out; export PYTHONUNBUFFERED=1
-for v in 0 $VARIANTS; do
+for round in $(seq ${ROUNDS:-1}); do for v in 0 $VARIANTS; do
   lib=""; [ $v -gt 0 ] && lib="$(pwd)/nem-mcmc-optimization_amd/nemo/libnemo_abl$v.so"
   NEMO_LIBRARY=$lib timeout -k 10 300 python - <<PY || exit 1
 import sys, numpy as np
@@ -34,4 +34,4 @@ for _ in range(20): eng.score_dev(B, pos.data_ptr(), w01.data_ptr(), ll.data_ptr
 torch.cuda.synchronize(); ms, n = eng.timing_read()
 print(f"ablate=$v kernel {ms / n * 1e3:.1f} us per {B} evals")
 PY
-done
+done; done
