@@ -6,7 +6,7 @@ effect NEM (BASELINE.json metric, config C3; C4 = the same per GPU at N > 1).
 A step is one batched pass of the hot path over B = 2048 (pos, W)
 evaluations whose inputs are already resident in HBM, enqueued on one HIP
 stream through the C-ABI: for the default path (the staged C3 model has the
-NEM structure) that is ONE kernel, score_i8o_kernel: per evaluation the
+NEM structure) that is ONE kernel, score_i8l_kernel: per evaluation the
 fixed-point digits of Delta in LDS, the int8 MFMA contraction and the fp64
 log-sum-exp, with the effect sum finalized in-kernel.
 With N > 1 (torchrun, one rank per GPU) every rank evaluates its own B
@@ -263,14 +263,19 @@ def main():
             fpe = algorithmic_flops_per_eval(S, E, cap)
             ach = B * fpe / (kern_ms / 1e3) / 1e12
             fk = eng.get_option("fact_kernel")
-            i8o = S <= 64 and eng.get_option("i8o") > 0 and fk in (0, 7, 8)
-            i8 = S <= 64 and (i8o or fk in (4, 5, 6))
-            kname = ("score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on "
+            i8l = S <= 64 and eng.get_option("i8l") > 0 and fk in (0, 10, 11, 12, 13)
+            i8o = not i8l and S <= 64 and eng.get_option("i8o") > 0 and fk in (0, 7, 8)
+            i8 = S <= 64 and (i8l or i8o or fk in (4, 5, 6))
+            kname = ("score_i8l_kernel (x / ln 2 = Delta.D1 + U' + G exact in int8 fixed point on "
+                     "v_mfma_i32_16x16x64_i8, 7 digit slices; e^x assembled from the integer "
+                     "accumulators + table + degree-2 series; log-sum-exp offset by the null row)"
+                     if i8l else
+                     "score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on "
                      "v_mfma_i32_16x16x64_i8, fp64 cells, log-sum-exp offset by the null row)" if i8o else
                      "score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
                      "fp64 cells + fused log-sum-exp)" if i8 else
                      "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)")
-            tkey = "i8o" if i8o else ("i8" if i8 else "factored")
+            tkey = "i8l" if i8l else ("i8o" if i8o else ("i8" if i8 else "factored"))
             roof = {"bound": "mfma", "achieved": ach, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                     "frac": ach / F64_MFMA_PEAK_TF,
                     "traffic": load_traffic(f"{args.config}:{tkey}:b{B}"),

@@ -697,12 +697,16 @@ __device__ __forceinline__ double exp_acc(double x, const uint2* __restrict__ ta
 // (j << 9) (exp_acc's table), so (T_0 & ~511) + e.y is the high dword of
 // 2^(floor(y) + j/2048): no range reduction in f64.  The remainder
 // R = (T_0 & 511) 2^18 + T_1 (units of 2^-38, |R| < 2^28: one shift-add and
-// one conversion, exact) gives f = R 2^-38 ln 2 in (-2.2e-5, 3.6e-4) and a
-// degree-3 series e^f within 8e-16.  Per cell: 5 integer + 1 cvt + 4 f64 VALU
-// and one LDS read, against 4 + 2 + 9 for exp_acc on an f64 cell.
-constexpr double kL2A1 = 2.521654753072454e-12;    // 2^-38 ln 2
-constexpr double kL2A2 = 3.1793713468464492e-24;   // kL2A1^2 / 2
-constexpr double kL2A3 = 2.672425622852573e-36;    // kL2A1^3 / 6
+// one conversion, exact) gives f = R 2^-38 ln 2 in (-2.2e-5, 3.6e-4), where
+// a degree-2 polynomial in R interpolating e^f at the three Chebyshev nodes
+// of that interval is within 2.9e-13 (relative, alternating sign) -- below
+// the fixed-point truncation of the cell (~2^-38 per entry).  Per cell: ~8
+// integer + 1 cvt + 3 f64 VALU and one LDS read, against 4 + 2 + 9 for
+// exp_acc on an f64 cell.  Coefficients: Newton form through the nodes in
+// 50-digit decimal arithmetic, rounded to double.
+constexpr double kL2C0 = 1.0000000000000377;
+constexpr double kL2C1 = 2.521654728528023e-12;
+constexpr double kL2C2 = 3.179908378901339e-24;
 
 // split in three so a caller can keep several table reads in flight
 __device__ __forceinline__ uint64_t exp2_fx_load(uint32_t t0) {
@@ -718,9 +722,7 @@ __device__ __forceinline__ uint64_t exp2_fx_load(uint32_t t0) {
 }
 __device__ __forceinline__ double exp2_fx_series(uint32_t t0, int t1) {
   const double r = (double)(int)(((t0 & 511u) << 18) + (uint32_t)t1);
-  double p = fma(r, kL2A3, kL2A2);
-  p = fma(r, p, kL2A1);
-  return fma(r, p, 1.0);
+  return fma(r, fma(r, kL2C2, kL2C1), kL2C0);
 }
 __device__ __forceinline__ double exp2_fx_apply(uint32_t t0, uint64_t ev, double p, double acc) {
   const uint32_t hi = (t0 & ~511u) + (uint32_t)(ev >> 32);
@@ -1111,6 +1113,198 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
   }
 }
 
+// ---------------------------------------------------------------------------
+// score_i8s_kernel: score_i8l_kernel with the Delta digits stationary in
+// registers.  In score_i8l_kernel every wave walks all row blocks of its
+// tiles, re-reading the 7 x NR A fragments from LDS per tile (28 KB of LDS
+// reads per 16-effect tile at S = 64, next to the table reads): the LDS, not
+// the SIMDs, sets the pace.  Here wave w owns row block rb = w % NR for every
+// tile of its group of sets (grp = w / NR, NG = 8 / NR groups): its 7 A
+// fragments and G C-inits are loaded into registers once, after the prep.
+// Per tile a wave sums its 16 rows per effect column (4 cells per lane +
+// the row-group swaps) and posts the sums to LDS; after a block barrier per
+// set, one wave of the group (rotating) adds the NR row-block sums, forms
+// l = 1 + sum and the set's partial (product per lane over two tiles, one
+// log).  Partials are per set, as in score_i8l_kernel, so ll bits do not
+// depend on the batch size or the block split.
+// ---------------------------------------------------------------------------
+template <int NR>
+__global__ __launch_bounds__(8 * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8s_kernel(
+    int S, int E, int ntiles, int nsets, int split, int cap, double padg,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const int8_t* __restrict__ udig, const double* __restrict__ u0,
+    const double* __restrict__ nullsum, const void* __restrict__ tabs,
+    double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
+  constexpr int WAVES = 8;
+  constexpr int SPAD = NR * 16;
+  constexpr int NSL = 7;
+  constexpr int NG = WAVES / NR;                          // groups of row-block waves
+  extern __shared__ __attribute__((aligned(16))) double lds8[];
+  uint2* etab_o = (uint2*)lds8;                          // [kExpTabN] at LDS address 0
+  double2* ltab = (double2*)(etab_o + kExpTabN);         // [128] log table
+  double* elo_s = (double*)(ltab + 128);                 // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  EvalLds ev;
+  ev.G = ehi_s + SPAD;                                   // [SPAD]
+  int* gi = (int*)(ev.G + SPAD);                         // [2][SPAD] g0, g1
+  ev.perm = gi + 2 * SPAD;                               // [SPAD]
+  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][SPAD][4] swizzled (a_byte)
+  // after the A fragments are in registers the same region holds the
+  // row-block column sums: [NG][2 (parity)][8 tiles][NR][16] doubles (16 KB)
+  double* colsum = (double*)ev.A;
+
+  const int work = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
+  const int b = work / split;
+  const int part = work - b * split;
+  const int spb = (nsets + split - 1) / split;
+  const int s_begin = part * spb;
+  const int s_end = min(nsets, s_begin + spb);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int rb = w % NR, grp = w / NR;
+  const int col = lane & 15, rg = lane >> 4;
+
+  {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    const int4* src = (const int4*)tabs;
+    int4* dst = (int4*)lds8;
+    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+  }
+  i8_init_eval<SPAD, NSL, 4>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
+  __syncthreads();
+  {  // U' / ln 2 as the free diagonal "parent" i of child i
+    int8_t* A8 = (int8_t*)ev.A;
+    for (int k = tid; k < S * NSL; k += blockDim.x) {
+      const int i = k / NSL, sl = k - i * NSL;
+      A8[sl * SPAD * 64 + a_byte<4>(i, i)] = udig[i * 8 + sl];
+    }
+  }
+  {
+    constexpr int KB = 4;
+    const int npass = i8_npass(S, cap);
+    const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
+    for (int k0 = 0; k0 < my; k0 += KB)
+      i8o_prep_passes<SPAD, WAVES, KB, 4, true>(ev, k0, w, lane, S, cap, 0, w01 + (size_t)b * S * S,
+                                                elo_s, ehi_s, ltab);
+  }
+  __syncthreads();
+  for (int i = tid; i < SPAD; i += blockDim.x) {  // G + u0 as in score_i8l_kernel
+    const double g = i < S ? ev.G[i] + u0[i] : ev.G[i];
+    const double g0 = rint(g * kL2Scale);
+    gi[i] = (int)g0 + (1023 << 20);
+    gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 262144.0);
+  }
+  __syncthreads();
+  // this wave's row block: A fragments and G C-inits into registers
+  i32x4 af[NSL];
+  {
+    const i32x4* Al = ev.A + (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) af[sl] = Al[(sl * SPAD + 16 * rb) * 4];
+  }
+  const i32x4 c0 = ((const i32x4*)gi)[(16 * rb) / 4 + rg];
+  const i32x4 c1 = ((const i32x4*)gi)[(SPAD + 16 * rb) / 4 + rg];
+  __syncthreads();  // the A region becomes the column-sum buffer
+#if NEMO_I8_ABLATE & 32  // instrumented build (tools/ablate.sh): prep only, no tiles
+  if (s_end > 0) return;
+#endif
+
+  const i32x4* Bt = (const i32x4*)B8;
+  const int nsb = s_end > s_begin ? s_end - s_begin : 0;
+  const int niter = (nsb + NG - 1) / NG;  // uniform over the block
+  int tpre = 8 * (s_begin + grp);
+  i32x4 bc = Bt[(size_t)min(tpre, ntiles - 1) * kWave + lane];
+  for (int k = 0; k < niter; ++k) {
+    const int set = s_begin + k * NG + grp;
+    double* cs = colsum + (size_t)((grp * 2 + (k & 1)) * 8) * NR * 16;
+    if (set < s_end) {
+      const int t_end = min(ntiles, 8 * set + 8);
+      for (int t = 8 * set; t < t_end; ++t) {
+        // next tile of this wave (next set of the group after the last one)
+        const int tn = t + 1 < t_end ? t + 1 : 8 * (set + NG);
+        const i32x4 b1 = bc;
+        const i32x4 b64 = b1 << 6;
+        bc = Bt[(size_t)min(tn, ntiles - 1) * kWave + lane];
+        const i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+            af[1], b1, __builtin_amdgcn_mfma_i32_16x16x64_i8(af[0], b64, i32x4{0, 0, 0, 0}, 0, 0, 0), 0, 0, 0);
+        const i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+            af[3], b1, __builtin_amdgcn_mfma_i32_16x16x64_i8(af[2], b64, c0, 0, 0, 0), 0, 0, 0);
+        const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[4], b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        const i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+            af[6], b1, __builtin_amdgcn_mfma_i32_16x16x64_i8(af[5], b64, c1, 0, 0, 0), 0, 0, 0);
+        uint32_t t0[4];
+        uint64_t evt[4];
+        double pr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+          evt[g] = exp2_fx_load(t0[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+        double ls0 = 0.0, ls1 = 0.0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (g & 1) ls1 = exp2_fx_apply(t0[g], evt[g], pr[g], ls1);
+          else ls0 = exp2_fx_apply(t0[g], evt[g], pr[g], ls0);
+        }
+        const double v = rowsum4(ls0 + ls1);  // the row block's 16 rows, per column
+        if (lane < 16) cs[((t - 8 * set) * NR + rb) * 16 + col] = v;
+      }
+    }
+    __syncthreads();
+    if (set < s_end && rb == k % NR) {  // this set's partial: 8 tiles x 16 columns
+      double lp = 1.0;
+      int le = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tt = (lane >> 4) + 4 * h;
+        const int t = 8 * set + tt;
+        double l = 1.0;  // + e^0 of the null row
+#pragma unroll
+        for (int q = 0; q < NR; ++q) l += cs[(tt * NR + q) * 16 + col];
+        lp *= t < ntiles && t * 16 + col < E ? l : 1.0;
+        le += __builtin_amdgcn_frexp_exp(lp);
+        lp = __builtin_amdgcn_frexp_mant(lp);
+      }
+      const double v = wsum(log(lp) + (double)le * 0.69314718055994530942);
+      if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+    }
+  }
+  if (split == 1) {
+    __syncthreads();
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nsets, nsets, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
+}
+
+template <int NR>
+hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                        double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  const int nsets = (ntiles + 7) / 8;
+  const int slots = 256 * (NEMO_I8O_WAVES_PER_SIMD * 4 / 8);
+  int split = (slots + batch - 1) / batch;
+  split = split < 1 ? 1 : (split > nsets ? nsets : split);
+  const size_t region = std::max((size_t)7 * SPAD * 64, (size_t)16384);
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + region;
+  score_i8s_kernel<NR><<<dim3(batch * split), 8 * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+  *nparts = nsets;
+  *finalized = split == 1;
+  return hipGetLastError();
+}
+
 template <int NR, int WAVES>
 hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
@@ -1140,8 +1334,10 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
 #define NEMO_I8O(NRV)                                                                          \
   case NRV:                                                                                    \
     if (l2)                                                                                    \
-      return waves == 8 ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
-                        : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
+      return waves == 0 ? launch_i8s_t<NRV>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == 16 ? launch_i8l_t<NRV, 16>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
+                         : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                         : launch_i8o_t<NRV, 4, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \

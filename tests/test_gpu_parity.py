@@ -347,13 +347,13 @@ def test_factored_kernel_variants_agree(s, e):
         assert eng.get_option("i8o") == (2 if s <= 64 else 0)
         assert eng.get_option("i8l") == (1 if s <= 64 else 0)
         for fk, nodiag in ((1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (7, 1), (8, 1),
-                           (10, 0), (11, 0)):
+                           (10, 0), (11, 0), (12, 0), (13, 0)):
             eng.set_option("fact_kernel", fk)
             eng.set_option("i8o_nodiag", nodiag)
             ll = eng.score(pos, w01, cap=cap)
             # 10 / 11 carry the fraction of each entry to 2^-38 / ln 2 (7 slices;
             # DESIGN.md 3.1e): ~1e-9 at 64 x 2000, the others ~1e-11
-            tol = 1e-8 if fk in (10, 11) else 1e-9
+            tol = 1e-8 if fk >= 10 else 1e-9
             assert np.max(np.abs(ll - ref)) <= tol, (fk, cap)
             for c in (0, 11, 36):
                 assert eng.score(pos[c:c + 1], w01[c:c + 1], cap=cap)[0] == ll[c], (fk, cap)
@@ -418,10 +418,17 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     # give the same bits, and so do the natural-scale offset kernel's (7 / 8)
     # and the max-offset kernel's (4 / 6)
     assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
-    for fk in (10, 11):
+    for fk in (10, 11, 12):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
+    # the register-stationary kernel: its own bits (per-set sums in another
+    # order), independent of the batch too
+    eng.set_option("fact_kernel", 13)
+    st13 = eng.score(pos, w01)
+    assert np.max(np.abs(st13 - big)) <= 1e-8
+    for n in (1, 7, 64):
+        assert np.array_equal(eng.score(pos[:n], w01[:n]), st13[:n])
     eng.set_option("fact_kernel", 8)
     nat = eng.score(pos, w01)
     assert np.max(np.abs(nat - big)) <= 1e-8
