@@ -282,9 +282,14 @@ def main():
                     "kernel": kname, "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
                     "note": "achieved = the algorithmic fp64 contraction Delta.D1 over the permissible "
                             "pairs (2*P*E FLOP/eval) per kernel second, priced against the dense fp64 "
-                            "MFMA peak; the int8 kernels compute it exactly in 48-bit fixed point "
-                            "(DESIGN.md 3.1a) and are bound by the fp64 VALU of the log-sum-exp "
-                            "epilogue (S*E exps/eval), not by the matrix cores: see valu_bound",
+                            "MFMA peak (the arithmetic type of the path). The int8 kernels compute that "
+                            "contraction exactly in fixed point on the int8 matrix cores (score_i8l: 7 "
+                            "digit slices, 2^-38 / ln 2 per entry) and assemble e^x from the integer "
+                            "accumulators, so they can run faster than an fp64 MFMA contraction: frac "
+                            "> 1 means the reformulation beats the fp64 matrix roofline, not a "
+                            "measurement artefact. What binds is the SIMD issue of the VALU epilogue "
+                            "(S*E exps/eval) beside the MFMAs: valu_bound (PMC, profiles/valu.json; "
+                            "DESIGN.md 3.1e)",
                     "valu_bound": load_valu_bound(f"{args.config}:{tkey}:b{B}")}
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)

@@ -98,3 +98,78 @@ def test_int8_digit_expansion_exact():
             # pairs (64 d_2t + d_2t+1) and the int32 recombination stay exact
             pairs = [64 * digits[2 * t] + digits[2 * t + 1] for t in range(4)]
             assert all(abs(v) * 64 < 2 ** 18 for v in pairs)
+
+
+# --- score_i8l_kernel (nemo_factored_i8.hip): log2 fixed point -------------
+L2_SCALE = 1512775.3951951857          # 2^20 / ln 2 (kL2Scale)
+L2_C = (1.0000000000000377, 2.521654728528023e-12, 3.179908378901339e-24)  # kL2C0..2
+
+
+def l2_digits(d):
+    """i8l_digits: v = d 2^20 / ln 2 -> h = rint(v) (4 digits), l = rint((v - h) 2^18)
+    (3 digits), as the device writes them."""
+    hd = float(np.rint(d * L2_SCALE))
+    h = int(hd)
+    l = int(np.rint(fma(d, L2_SCALE, -hd) * 262144.0))
+    hb, lb = h + 32 * (1 + 64 + 4096), l + 32 * (1 + 64)
+    hd4 = [hb >> 18, ((hb >> 12) & 63) - 32, ((hb >> 6) & 63) - 32, (hb & 63) - 32]
+    ld3 = [lb >> 12, ((lb >> 6) & 63) - 32, (lb & 63) - 32]
+    return h, l, hd4, ld3
+
+
+def test_log2_digit_expansion_exact():
+    """h 2^-20 + l 2^-38 is d / ln 2 within 2^-39 (+ the rounding of d * kL2Scale);
+    the 7 slices are int8 (top digit of h in [-128, 127] up to |d| / ln 2 < 31.87,
+    the others in [-32, 32]); the MFMA pairs rebuild h and l exactly."""
+    rng = np.random.default_rng(3)
+    ds = np.concatenate([rng.uniform(-1, 1, 400) * 5.2, rng.uniform(-22.0, 22.0, 200), [0.0, 1e-12, -3.7]])
+    for d in ds:
+        h, l, hd4, ld3 = l2_digits(float(d))
+        assert -128 <= hd4[0] <= 127 and all(-32 <= q <= 31 for q in hd4[1:])
+        assert -32 <= ld3[0] <= 32 and all(-32 <= q <= 31 for q in ld3[1:])
+        assert (64 * hd4[0] + hd4[1]) * 4096 + (64 * hd4[2] + hd4[3]) == h
+        assert ld3[0] * 4096 + (64 * ld3[1] + ld3[2]) == l
+        back = Fraction(h) / 2 ** 20 + Fraction(l) / 2 ** 38
+        ref = mpmath.mpf(float(d)) / mpmath.log(2)
+        assert abs(mpmath.mpf(back.numerator) / back.denominator - ref) <= 2.0 ** -39 + abs(float(d)) * 2.0 ** -52
+
+
+def _l2_table():
+    tab = []
+    for j in range(2048):
+        v = float(mpmath.mpf(2) ** (mpmath.mpf(j) / 2048))
+        b = int(np.float64(v).view(np.uint64))
+        tab.append((b & 0xFFFFFFFF, (((b >> 32) & 0x800FFFFF) - (j << 9)) & 0xFFFFFFFF))
+    return tab
+
+
+def exp2_fx(t0, t1, tab):
+    """exp2_fx_load / _series / _apply on (T_0, T_1) with 32-bit integer semantics."""
+    t0 &= 0xFFFFFFFF
+    low = t0 & 511
+    lo, hi_t = tab[(t0 >> 6 & 0x3FF8) >> 3]
+    hi = ((t0 & ~511 & 0xFFFFFFFF) + hi_t) & 0xFFFFFFFF
+    value = float(np.uint64((hi << 32) | lo).view(np.float64))
+    r32 = ((low << 18) + t1) & 0xFFFFFFFF
+    r = float(r32 - (1 << 32) if r32 >= 1 << 31 else r32)
+    p = fma(r, fma(r, L2_C[2], L2_C[1]), L2_C[0])
+    return value * p
+
+
+def test_exp2_fixed_point_assembly():
+    """2^y from the integer accumulators, y = (T_0 - 1023 2^20) 2^-20 + T_1 2^-38:
+    table entry with the exponent added to its high dword, remainder through the
+    degree-2 Chebyshev series; within 3e-13 relative over the staged range
+    (|y| <= 995.5, |T_1| <= 65 2^17)."""
+    tab = _l2_table()
+    rng = np.random.default_rng(4)
+    worst = 0.0
+    for _ in range(1500):
+        y_int = int(rng.integers(-995, 995))
+        frac = int(rng.integers(0, 1 << 20))
+        t1 = int(rng.integers(-65 * 2 ** 17, 65 * 2 ** 17 + 1))
+        t0 = (1023 + y_int) * 2 ** 20 + frac
+        y = mpmath.mpf(y_int) + mpmath.mpf(frac) / 2 ** 20 + mpmath.mpf(t1) / 2 ** 38
+        ref = mpmath.mpf(2) ** y
+        worst = max(worst, float(abs(mpmath.mpf(exp2_fx(t0, t1, tab)) / ref - 1)))
+    assert worst <= 3.2e-13

@@ -18,7 +18,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        for tag, kind in (("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+        for tag, kind in (("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
                           ("score_factored_kernel", "factored"), ("score_kernel", "stream")):
             if tag in name:
                 agg[kind].append(float(r["Counter_Value"]))

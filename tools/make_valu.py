@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-TAGS = (("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+TAGS = (("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
         ("score_factored_kernel", "factored"), ("score_kernel", "stream"))
 
 
@@ -34,8 +34,18 @@ def main():
         m = {k: sum(v) / len(v) for k, v in d.items()}
         rec = {k: m[k] for k in sorted(m)}
         if "SQ_ACTIVE_INST_VALU" in m and "GRBM_GUI_ACTIVE" in m:
-            rec["valu_busy"] = 4.0 * m["SQ_ACTIVE_INST_VALU"] / (1024.0 * m["GRBM_GUI_ACTIVE"] / 8.0)
-        rec["formula"] = "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)"
+            simd_cyc = 1024.0 * m["GRBM_GUI_ACTIVE"] / 8.0
+            rec["valu_busy"] = 4.0 * m["SQ_ACTIVE_INST_VALU"] / simd_cyc
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                rec["mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cyc
+            if "SQ_VALU_MFMA_COEXEC_CYCLES" in m:
+                rec["mfma_coexec_frac"] = m["SQ_VALU_MFMA_COEXEC_CYCLES"] / max(m.get("SQ_VALU_MFMA_BUSY_CYCLES", 1.0), 1.0)
+            if "SQ_LDS_IDX_ACTIVE" in m:
+                rec["lds_busy"] = m["SQ_LDS_IDX_ACTIVE"] / (256.0 * m["GRBM_GUI_ACTIVE"] / 8.0)
+        rec["formula"] = ("valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); "
+                          "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / the same; mfma_coexec_frac = "
+                          "SQ_VALU_MFMA_COEXEC_CYCLES / SQ_VALU_MFMA_BUSY_CYCLES (MFMA cycles with a VALU "
+                          "issue beside them); lds_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE / 8)")
         data[prefix.replace("{kind}", kind)] = rec
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data, indent=1))
