@@ -133,6 +133,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  if (c.h_stage) (void)hipHostFree(c.h_stage);
   for (hipEvent_t ev : c.ev_pool) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(c.stream);
   delete ctx;
@@ -180,6 +181,20 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
 }  // extern "C"
 
 namespace {
+
+// grow the pinned host staging buffer to at least `bytes`
+int host_stage(Ctx& c, size_t bytes) {
+  if (bytes <= c.h_stage_bytes) return NEMO_OK;
+  HIPCHK(hipStreamSynchronize(c.stream));
+  if (c.h_stage) {
+    HIPCHK(hipHostFree(c.h_stage));
+    c.h_stage = nullptr;
+    c.h_stage_bytes = 0;
+  }
+  HIPCHK(hipHostMalloc(&c.h_stage, bytes, hipHostMallocDefault));
+  c.h_stage_bytes = bytes;
+  return NEMO_OK;
+}
 
 // (re)allocate the table buffers of a staging: exp(T) and U in the table
 // dtype, U in fp64 padded to the factored row blocking (the int8 kernel reads
@@ -621,25 +636,39 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
   Ctx& c = ctx->c;
   if ((rc = check_pos(pos, nchains, c.S))) return rc;
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
-  const size_t S = c.S;
+  const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
-  HIPCHK(hipMemcpyAsync(c.d_pos, pos, nchains * S * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c.d_w01, w01, nchains * S * S * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c.d_anc, anc, nchains * S * S * 8, hipMemcpyHostToDevice, st));
-  // entries outside the permissible pairs keep the caller's values
-  HIPCHK(hipMemcpyAsync(c.d_wnew, w_new, nchains * S * S * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(c.d_info, 0xff, nchains * S * S * 4, st));
+  // every transfer goes through the pinned staging buffer: [pos | w01 | anc |
+  // w_new | info | ll1 | ll_dag], each part 256-B aligned
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t o_w01 = up(n * S * 4), o_anc = o_w01 + up(n * S * S * 8), o_wn = o_anc + up(n * S * S * 8),
+               o_inf = o_wn + up(n * S * S * 8), o_ll1 = o_inf + up(n * S * S * 4), o_lld = o_ll1 + up(n * 8),
+               total = o_lld + up(n * 8);
+  if ((rc = host_stage(c, total))) return rc;
+  char* hs = (char*)c.h_stage;
+  memcpy(hs, pos, n * S * 4);
+  memcpy(hs + o_w01, w01, n * S * S * 8);
+  memcpy(hs + o_anc, anc, n * S * S * 8);
+  memcpy(hs + o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
+  HIPCHK(hipMemcpyAsync(c.d_pos, hs, n * S * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_w01, hs + o_w01, n * S * S * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_anc, hs + o_anc, n * S * S * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c.d_wnew, hs + o_wn, n * S * S * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemsetAsync(c.d_info, 0xff, n * S * S * 4, st));
   rc = nemo_optimal_weights_dev(ctx, nchains, c.d_pos, c.d_w01, c.d_anc, sig0, sig1, cap, c.d_wnew,
                                 c.d_ll, c.d_ll2, c.d_info, st);
   if (rc) return rc;
-  std::vector<int32_t> inf(nchains * S * S);
-  HIPCHK(hipMemcpyAsync(w_new, c.d_wnew, nchains * S * S * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(ll1, c.d_ll, nchains * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(ll_dag, c.d_ll2, nchains * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(inf.data(), c.d_info, inf.size() * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + o_wn, c.d_wnew, n * S * S * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + o_ll1, c.d_ll, n * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + o_lld, c.d_ll2, n * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + o_inf, c.d_info, n * S * S * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (info) memcpy(info, inf.data(), inf.size() * 4);
-  for (size_t k = 0; k < inf.size(); ++k) {
+  memcpy(w_new, hs + o_wn, n * S * S * 8);
+  memcpy(ll1, hs + o_ll1, n * 8);
+  memcpy(ll_dag, hs + o_lld, n * 8);
+  if (info) memcpy(info, hs + o_inf, n * S * S * 4);
+  const int32_t* inf = (const int32_t*)(hs + o_inf);
+  for (size_t k = 0; k < n * S * S; ++k) {
     if (inf[k] == -1) continue;  // not a permissible pair
     const int status = inf[k] & 15;
     if (status >= NEMO_LBFGSB_ABNORMAL) {

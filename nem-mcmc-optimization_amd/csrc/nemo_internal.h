@@ -108,6 +108,12 @@ struct Ctx {
   double* d_gsw = nullptr;
   int32_t* d_gcnt = nullptr;
 
+  // pinned host staging of the host-pointer entry points (hipHostMalloc):
+  // pageable hipMemcpyAsync blocks the host ~0.1 ms per 512 KB, a memcpy into
+  // pinned memory plus a DMA copy costs a fraction of that
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
+
   // timing of the score kernel
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
