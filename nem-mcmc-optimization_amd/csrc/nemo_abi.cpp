@@ -260,6 +260,11 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
             if (k < S) b8[(t * 64 + l) * 16 + jj] = (uint8_t)((d1[k * nwords + e / 64] >> (e % 64)) & 1ull);
           }
         }
+      // a second copy scaled by 64 follows (the B operand of the high digit of
+      // each pair; score_i8l_kernel loads it instead of shifting per tile)
+      const size_t nb = b8.size();
+      b8.resize(2 * nb);
+      for (size_t k = 0; k < nb; ++k) b8[nb + k] = (uint8_t)(b8[k] << 6);
       HIPCHK(hipMalloc((void**)&c.d_B8, b8.size()));
       HIPCHK(hipMemcpy(c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
     }

@@ -1023,6 +1023,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
 #endif
 
   const i32x4* Bt = (const i32x4*)B8;
+  const i32x4* Bt64 = Bt + (size_t)ntiles * kWave;  // the staged D1 bytes x 64
   const i32x4* Gi = (const i32x4*)gi;
   const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
   int set = s_begin + w;
@@ -1031,6 +1032,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
     int lexp = 0;
     int t = 8 * set;
     i32x4 bc = Bt[(size_t)t * kWave + lane];
+    i32x4 bc64 = Bt64[(size_t)t * kWave + lane];
     for (;;) {
       uint32_t ao = a_lane;
       asm volatile("" : "+v"(ao));
@@ -1042,9 +1044,9 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_
       }
       const bool more = setn < s_end;
       const int tl = more ? tn : t;  // prefetch target (the current tile again at the end)
-      const i32x4 b1 = bc;
-      const i32x4 b64 = b1 << 6;
+      const i32x4 b1 = bc, b64 = bc64;
       bc = Bt[(size_t)tl * kWave + lane];
+      bc64 = Bt64[(size_t)tl * kWave + lane];
       double ls0 = 0.0, ls1 = 0.0;
 #pragma unroll
       for (int r = 0; r < NR; ++r) {

@@ -73,7 +73,8 @@ struct Ctx {
   double* d_fpartial = nullptr;    // [cap][factored_partials]
   // int8 matrix-core variant (S <= 64): fixed-point Delta digits
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
-  uint8_t* d_B8 = nullptr;         // [ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
+  uint8_t* d_B8 = nullptr;         // [2][ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order,
+                                   // then the same x 64
   // offset log-sum-exp variant (score_i8o_kernel), staged by stage_i8o
   bool i8o_ok = false;             // staging bounds hold: |cell - U[S]| <= 690
   double i8o_padg = 0.0;           // G of padding rows
