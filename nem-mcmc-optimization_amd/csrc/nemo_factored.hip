@@ -531,12 +531,13 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   if (cap >= c.S - 1) cap = 0;  // every predecessor is within the cap: no cap (same bits)
   const bool ll_only0 = !d_cs && !d_cells && !d_ow;
-  // capped ll-only calls: the banded lookup-table kernel (fact_kernel 9; auto
-  // when staged), which derives its tables itself
+  // capped ll-only calls: the banded lookup-table kernel (fact_kernel 9, its
+  // round-1 form with the row bits re-read from LDS 15; auto when staged),
+  // which derives its tables itself
   const bool win = ll_only0 && c.win_ok && cap >= 1 && cap <= kWinMaxCap &&
-                   (c.fact_kernel == 0 || c.fact_kernel == 9);
-  if (c.fact_kernel == 9 && !win) return hipErrorInvalidValue;
-  const bool i8_path = spad <= 64 && ((fk0 >= 4 && fk0 <= 8) || (fk0 >= 10 && fk0 <= 13)) && ll_only0 && c.d_B8;
+                   (c.fact_kernel == 0 || c.fact_kernel == 9 || c.fact_kernel == 15);
+  if ((c.fact_kernel == 9 || c.fact_kernel == 15) && !win) return hipErrorInvalidValue;
+  const bool i8_path = spad <= 64 && ((fk0 >= 4 && fk0 <= 8) || (fk0 >= 10 && fk0 <= 14)) && ll_only0 && c.d_B8;
   hipError_t err = hipSuccess;
   if (!i8_path && !win) {  // the int8 kernel derives its Delta digits itself
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
@@ -554,21 +555,22 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,
   // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves,
   // 7 / 8 int8 with the offset log-sum-exp (4 / 8 waves), 10 / 11 the same in
-  // log2 fixed point (8 / 4 waves; 12: 16 waves); auto prefers 10, then 8
+  // log2 fixed point (8 / 4 waves; 12: 16 waves; 13: register-stationary;
+  // 14: 8 waves compiled for 6 waves per SIMD); auto prefers 10, then 8
   const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool ll_only = !d_cs && !d_cells && !d_ow;
   const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
-  const bool i8 = spad <= 64 && ((fk >= 4 && fk <= 8) || (fk >= 10 && fk <= 13)) && ll_only && c.d_B8;
+  const bool i8 = spad <= 64 && ((fk >= 4 && fk <= 8) || (fk >= 10 && fk <= 14)) && ll_only && c.d_B8;
   int np = 0;
   bool finalized = false;
   const bool l2 = i8 && c.i8o_ok && c.i8l_ok && (fk >= 10 || c.fact_kernel == 0);
   const bool i8o = i8 && c.i8o_ok && (fk == 7 || fk == 8 || c.fact_kernel == 0 || l2);
   if (win) {
-    err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized);
+    err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized, c.fact_kernel == 15);
   } else if (i8o) {
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block, 10 / 11: log2
     // fixed point with 8 / 4 (auto: 8)
-    const int waves = fk == 13 ? 0 : (fk == 12 ? 16 : ((fk == 7 || fk == 11) ? 4 : 8));
+    const int waves = fk == 13 ? 0 : fk == 14 ? -8 : (fk == 12 ? 16 : ((fk == 7 || fk == 11) ? 4 : 8));
     err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, l2, st, &np, &finalized);
   } else if (i8 && fk <= 6) {
     // auto: 4 waves per block for large batches, 8 (fewer splits) below

@@ -948,8 +948,8 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
 // units 2^-38): 7 MFMAs per row block against 8.  Requires the diagonal form
 // (stage_i8o).
 // ---------------------------------------------------------------------------
-template <int NR, int WAVES>
-__global__ __launch_bounds__(WAVES * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8l_kernel(
+template <int NR, int WAVES, int OCC>
+__global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
     const double* __restrict__ e_lo, const double* __restrict__ e_hi,
@@ -1307,17 +1307,17 @@ hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   return hipGetLastError();
 }
 
-template <int NR, int WAVES>
+template <int NR, int WAVES, int OCC = NEMO_I8O_WAVES_PER_SIMD>
 hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
   const int ntiles = (c.E + 15) / 16;
   const int nsets = (ntiles + 7) / 8;
-  const int slots = 256 * (NEMO_I8O_WAVES_PER_SIMD * 4 / WAVES);
+  const int slots = 256 * (OCC * 4 / WAVES);
   int split = (slots + batch - 1) / batch;
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)7 * SPAD * 64;
-  score_i8l_kernel<NR, WAVES><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+  score_i8l_kernel<NR, WAVES, OCC><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
       c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
@@ -1339,6 +1339,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
       return waves == 0 ? launch_i8s_t<NRV>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 16 ? launch_i8l_t<NRV, 16>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
+           : waves == -8 ? launch_i8l_t<NRV, 8, 6>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                          : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \

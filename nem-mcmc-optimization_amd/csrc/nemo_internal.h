@@ -176,7 +176,8 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
 // capped lookup-table kernel (nemo_window.hip): ll only, 1 <= cap <= kWinMaxCap,
 // S <= kWinMaxS; one partial per 64-effect word (*nparts = nwords)
 hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                               double* d_ll, hipStream_t st, int* nparts, bool* finalized);
+                               double* d_ll, hipStream_t st, int* nparts, bool* finalized,
+                               bool walk_lds = false);
 hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
                         const std::vector<uint64_t>& d1);
 

@@ -144,12 +144,255 @@ __global__ __launch_bounds__(WAVES * kWave) void score_window_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// score_window2_kernel: the same tables, walked from registers.
+//
+// Per 64-effect word a wave loads the D1 words of its rows in ORDER position
+// (lane r: row r, r + 64, ...) and transposes each 64 x 64 bit block across
+// the lanes (one v_permlane32_swap, then five butterfly stages of a partner
+// fetch, a rotate and a bit select), so lane e holds R = the bits of effect e
+// over the order positions, 32 rows per dword.  The window of row q -- the
+// bits of rows q-6 .. q -- is then one funnel shift of two of those dwords:
+//     X_q = (R >> (q - 6)) (32 bits),  bits 3..6 = rows q-3 .. q,
+// so X_q & 0x78 is directly the byte offset of row q's A entry (own bit and
+// parents 1-3, 16 entries).  Parents 4-6 of row q are rows q-6 .. q-4, the
+// low three bits of row q-3's A index: row q's second table B' is stored with
+// 16 entries (B'[m] = B[m & 7]) and read at row q-3's A offset.  Row q's tables
+// sit at q * 256 bytes (A, then B'), so with the rows unrolled every table
+// offset is an instruction immediate and a cell costs one shift, one AND, two
+// LDS reads and one FMA (against ~9 VALU and three LDS reads in
+// score_window_kernel, which re-extracts each row's bit from an LDS word).
+// Tables are products of the per-parent factors 1 - w + w e^{T} (the terms
+// whose logs the cell sums) and e^{U'}: no log or exp per entry.
+// ---------------------------------------------------------------------------
+constexpr int kWin2Row = 256;  // bytes of tables per row: A[16] and B'[16], in two regions
+#ifndef NEMO_WIN2_OCC
+#define NEMO_WIN2_OCC 6
+#endif
+#ifndef NEMO_WIN2_CHUNK
+#define NEMO_WIN2_CHUNK 8
+#endif  // bytes of one row's tables (A[16], B'[16])
+
+__host__ __device__ __forceinline__ size_t win2_lds_bytes(int S) {
+  const int rows = 64 * ((S + 63) / 64);
+  return (size_t)rows * kWin2Row + 64 + 128 * 16 + (size_t)S * 4;
+}
+
+__device__ __forceinline__ double lds_f64(uint32_t addr) {
+  return *(const __attribute__((address_space(3))) double*)(size_t)addr;
+}
+
+// value of lane ^ D (D < 32) within 32-lane halves
+template <int D>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (D == 1) return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  else if constexpr (D == 2) return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+  else if constexpr (D == 8) return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (D << 10));  // bit mode, xor D
+}
+
+// one butterfly stage of the 32 x 32 transpose (lane = row, bit = column):
+// the lane with bit D clear keeps its columns with bit D clear and takes the
+// partner's (shifted up by D), the other one the reverse (tests/test_numerics.py
+// restates it)
+template <int D>
+__device__ __forceinline__ uint32_t tr_stage(uint32_t x, uint32_t sh, uint32_t m) {
+  const uint32_t p = lane_xor<D>(x);
+  const uint32_t rot = __builtin_amdgcn_alignbit(p, p, sh);
+  return (x & m) | (rot & ~m);
+}
+
+template <int NB, int WAVES>
+__global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_kernel(
+    int S, int E, int nwords, int cap, int split, const int32_t* __restrict__ pos,
+    const double* __restrict__ w01, const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint64_t* __restrict__ D1w, const double* __restrict__ uw, const double* __restrict__ nullw,
+    double* __restrict__ partial, double* __restrict__ ll_out) {
+  constexpr int ROWS = 64 * NB;
+  // B' region: 64 B past the A rows, so no A / B' read pair is a multiple of
+  // 512 B apart (the compiler would fuse it into ds_read2st64_b64, which moves
+  // 128 B/clk against 256 for two ds_read_b64)
+  constexpr int kB0 = ROWS * 128 + 64;
+  extern __shared__ __attribute__((aligned(16))) double ldsw[];
+  double* lut = ldsw;                                  // at LDS address 0: [ROWS][A 16 | B' 16]
+  double2* ltab = (double2*)(ldsw + (size_t)ROWS * 32 + 8);  // log_fast's table
+  int* perm = (int*)(ltab + 128);                      // [S] node at each order position
+
+  const int b = blockIdx.x / split;
+  const int part = blockIdx.x - b * split;
+  const int wpb = (nwords + split - 1) / split;
+  const int wbeg = part * wpb, wend = min(nwords, wbeg + wpb);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int nt = blockDim.x;
+
+  for (int k = tid; k < S; k += nt) perm[k] = 0;
+  fill_log_table(ltab, tid, nt);
+  __syncthreads();
+  for (int i = tid; i < S; i += nt) {
+    int p = pos[(size_t)b * S + i];
+    p = p < 0 ? 0 : (p >= S ? S - 1 : p);  // malformed input must not fault (the ABI validates)
+    perm[p] = i;
+  }
+  __syncthreads();
+  // one thread per row: y[d][bit] = 1 - w + w e^{T} of parent q-d (d = 1..6;
+  // 1 past the cap / the order start), y[0][bit] = e^{U'} of the row's own bit
+  const double* wb = w01 + (size_t)b * S * S;
+  for (int q = tid; q < ROWS; q += nt) {
+    double* a = lut + (size_t)q * 16;            // A rows at 128 q
+    double* bq = lut + (size_t)kB0 / 8 + (size_t)q * 16;  // B' rows at kB0 + 128 q
+    if (q >= S) {  // padding rows: A = 0 adds nothing
+#pragma unroll
+      for (int m = 0; m < 16; ++m) a[m] = bq[m] = 0.0;
+      continue;
+    }
+    const int i = perm[q];
+    double y[7][2];
+    y[0][0] = exp(uw[2 * i]);
+    y[0][1] = exp(uw[2 * i + 1]);
+#pragma unroll
+    for (int d = 1; d <= 6; ++d) {
+      y[d][0] = 1.0;
+      y[d][1] = 1.0;
+      if (d <= cap && q >= d) {
+        const int j = perm[q - d];
+        const double s = wb[(size_t)i * S + j];
+        y[d][0] = fma(s, e_lo[j] - 1.0, 1.0);
+        y[d][1] = fma(s, e_hi[j] - 1.0, 1.0);
+      }
+    }
+    // A index bits 0..3 = rows q-3, q-2, q-1, q; B' index bits 0..2 = rows q-6, q-5, q-4
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      a[m] = ((y[0][(m >> 3) & 1] * y[1][(m >> 2) & 1]) * y[2][(m >> 1) & 1]) * y[3][m & 1];
+      bq[m] = (y[4][(m >> 2) & 1] * y[5][(m >> 1) & 1]) * y[6][m & 1];
+    }
+  }
+  __syncthreads();
+
+  // per-lane constants of the five butterfly stages (D = 16 .. 1)
+  constexpr uint32_t kMlo[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
+  uint32_t tsh[5], tm[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int d = 16 >> k;
+    const bool up = (lane & d) != 0;
+    tsh[k] = up ? (uint32_t)d : (uint32_t)(32 - d);
+    tm[k] = up ? ~kMlo[k] : kMlo[k];
+  }
+  for (int word = wbeg + w; word < wend; word += WAVES) {
+    uint32_t R[2 * NB];
+#pragma unroll
+    for (int blk = 0; blk < NB; ++blk) {
+      const int r = 64 * blk + lane;
+      const uint64_t v = r < S ? D1w[(size_t)perm[r] * nwords + word] : 0ull;
+      uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+      // lanes 0-31: high dwords <-> lanes 32-63: low dwords (the off-diagonal 32 x 32 blocks)
+      const auto sw = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+      lo = sw[0];
+      hi = sw[1];
+      lo = tr_stage<16>(lo, tsh[0], tm[0]);
+      hi = tr_stage<16>(hi, tsh[0], tm[0]);
+      lo = tr_stage<8>(lo, tsh[1], tm[1]);
+      hi = tr_stage<8>(hi, tsh[1], tm[1]);
+      lo = tr_stage<4>(lo, tsh[2], tm[2]);
+      hi = tr_stage<4>(hi, tsh[2], tm[2]);
+      lo = tr_stage<2>(lo, tsh[3], tm[3]);
+      hi = tr_stage<2>(hi, tsh[3], tm[3]);
+      lo = tr_stage<1>(lo, tsh[4], tm[4]);
+      hi = tr_stage<1>(hi, tsh[4], tm[4]);
+      R[2 * blk] = lo;      // rows 64 blk + 0..31 of effect 64 word + lane
+      R[2 * blk + 1] = hi;  // rows 64 blk + 32..63
+    }
+    // rows in 32-row groups (a runtime loop, so the scheduler sees one group
+    // at a time); av = (X & 0x78) | 4096 g, so A(q) is at av + 128 t and
+    // B'(q) at av(q-3) + kB0 + 128 t(q-3) + 384 (t = row within its group)
+    double s0 = 0.0, s1 = 0.0;
+    uint32_t ap0 = (uint32_t)-4096, ap1 = ap0, ap2 = ap0;  // rows -3..-1: group -1, index 0
+    uint32_t Rp = 0u, Rc = R[0];
+#pragma unroll 1
+    for (int g = 0; g < 2 * NB; ++g) {
+      // the group base in a VGPR (opaque), so each row's offset is one bit
+      // select (X & 0x78) | (gv & ~0x78) instead of an AND and an add
+      uint32_t gv = (uint32_t)g << 12;
+      asm volatile("" : "+v"(gv));
+      uint32_t av[32];
+      // 8 rows at a time: 16 reads in flight, then the FMAs
+#pragma unroll
+      for (int t0 = 0; t0 < 32; t0 += 8) {
+        double A[8], B[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int t = t0 + u;
+          const uint32_t X = t >= 6 ? Rc >> (t - 6) : __builtin_amdgcn_alignbit(Rc, Rp, t + 26);
+          av[t] = (X & 0x78u) | (gv & ~0x78u);
+          const uint32_t aq3 = t >= 3 ? av[t >= 3 ? t - 3 : 0] : (t == 0 ? ap0 : (t == 1 ? ap1 : ap2));
+          A[u] = lds_f64(av[t] + (uint32_t)(t * 128));
+          // aq3 holds row q-3's group base and index only: add its row within
+          // that group (t - 3, or t + 29 for the previous group) and 3 rows
+          B[u] = lds_f64(aq3 + (uint32_t)(kB0 + 128 * (t >= 3 ? t - 3 : t + 29) + 384));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (u & 1) s1 = fma(A[u], B[u], s1);
+          else s0 = fma(A[u], B[u], s0);
+        }
+      }
+      ap0 = av[29];
+      ap1 = av[30];
+      ap2 = av[31];
+      Rp = Rc;
+      // next group's dword (R shifts down one: a compile-time rotation)
+#pragma unroll
+      for (int k = 0; k + 1 < 2 * NB; ++k) R[k] = R[k + 1];
+      Rc = R[0];
+    }
+    double v = 64 * word + lane < E ? log_fast(1.0 + (s0 + s1), ltab) : 0.0;  // 1 = e^0 of the null row
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    if (lane == 0) partial[(size_t)b * nwords + word] = nullw[word] + v;
+  }
+  if (split == 1) {
+    __syncthreads();
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)b * nwords, nwords, lane);
+      if (lane == 0) ll_out[b] = v;
+    }
+  }
+}
+
+template <int NB>
+hipError_t launch_window2_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, hipStream_t st, int split) {
+  score_window2_kernel<NB, kWinWaves><<<dim3(batch * split), kWinWaves * kWave, win2_lds_bytes(c.S), st>>>(
+      c.S, c.E, c.nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
+      c.d_fpartial, d_ll);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                               double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+                               double* d_ll, hipStream_t st, int* nparts, bool* finalized, bool walk_lds) {
   if (!c.win_ok || cap < 1 || cap > kWinMaxCap || c.S > kWinMaxS) return hipErrorInvalidValue;
   const int nwords = c.nwords;
+  if (!walk_lds) {
+    // 3 blocks per CU (LDS at S = 128, 80 VGPRs)
+    int split = (768 + batch - 1) / batch;
+    split = std::max(1, std::min(split, (nwords + kWinWaves - 1) / kWinWaves));
+    hipError_t err;
+    switch ((c.S + 63) / 64) {
+      case 1: err = launch_window2_t<1>(c, batch, cap, d_pos, d_w01, d_ll, st, split); break;
+      case 2: err = launch_window2_t<2>(c, batch, cap, d_pos, d_w01, d_ll, st, split); break;
+      case 3: err = launch_window2_t<3>(c, batch, cap, d_pos, d_w01, d_ll, st, split); break;
+      case 4: err = launch_window2_t<4>(c, batch, cap, d_pos, d_w01, d_ll, st, split); break;
+      default: return hipErrorInvalidValue;
+    }
+    *nparts = nwords;
+    *finalized = split == 1;
+    return err;
+  }
   // enough blocks to fill 256 CUs (LDS allows 3 per CU at S = 128); every
   // word's partial is the same whatever the split, so bits do not depend on it
   const int slots = 768;

@@ -173,3 +173,91 @@ def test_exp2_fixed_point_assembly():
         ref = mpmath.mpf(2) ** y
         worst = max(worst, float(abs(mpmath.mpf(exp2_fx(t0, t1, tab)) / ref - 1)))
     assert worst <= 3.2e-13
+
+
+# --- score_window2_kernel (nemo_window.hip): register walk of the capped tables ---
+
+_MLO = {16: 0x0000FFFF, 8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
+
+
+def _rotr(x, s):
+    x = x.astype(np.uint64)
+    s = np.asarray(s, dtype=np.uint64)
+    return (((x >> s) | (x << ((np.uint64(32) - s) % np.uint64(32)))) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def window_transpose(m):
+    """The kernel's cross-lane transpose of a 64 x 64 bit block (lane r holds
+    row r as lo / hi dwords): the v_permlane32_swap of the off-diagonal 32 x 32
+    blocks, then the five butterfly stages of tr_stage (partner = lane ^ d, a
+    rotate by d or 32 - d, a bit select by the stage mask)."""
+    lo = (m & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    hi = (m >> np.uint64(32)).astype(np.uint32)
+    lo2, hi2 = lo.copy(), hi.copy()
+    lo2[32:], hi2[:32] = hi[:32], lo[32:]
+    lo, hi = lo2, hi2
+    lane = np.arange(64)
+    for d in (16, 8, 4, 2, 1):
+        up = (lane & d) != 0
+        sh = np.where(up, d, 32 - d)
+        msk = np.where(up, ~np.uint32(_MLO[d]), np.uint32(_MLO[d])).astype(np.uint32)
+        lo = ((lo & msk) | (_rotr(lo[lane ^ d], sh) & ~msk)).astype(np.uint32)
+        hi = ((hi & msk) | (_rotr(hi[lane ^ d], sh) & ~msk)).astype(np.uint32)
+    return lo, hi
+
+
+def test_window_transpose_is_a_transpose():
+    rng = np.random.default_rng(3)
+    m = rng.integers(0, 2**64, size=64, dtype=np.uint64)
+    lo, hi = window_transpose(m)
+    bits = (m[:, None] >> np.arange(64, dtype=np.uint64)[None, :]) & np.uint64(1)  # [row][col]
+    for j in range(64):
+        assert int(lo[j]) == sum(int(bits[t, j]) << t for t in range(32))
+        assert int(hi[j]) == sum(int(bits[32 + t, j]) << t for t in range(32))
+
+
+@pytest.mark.parametrize("s,cap", [(128, 6), (70, 3), (11, 6), (5, 6), (33, 1), (150, 5)])
+def test_window_walk_offsets(s, cap):
+    """The kernel's LDS offsets, restated: A rows at 128 q, B' rows at
+    kB0 + 128 q (B'[m] = B[m & 7]), av = (X & 0x78) | 4096 g from the funnel
+    shift X of the transposed bits, B'(q) read at row q-3's av.  The walk must
+    give sum_q e^{U'} prod_d y_d for every effect, rows before the order
+    start and past the cap contributing factor 1."""
+    rng = np.random.default_rng(s + cap)
+    nb = (s + 63) // 64
+    rows, kb0, mask = 64 * nb, 64 * nb * 128 + 64, 0xFFFFFFFF
+    perm = rng.permutation(s)
+    bits = rng.integers(0, 2, size=(s, 64))
+    y = rng.uniform(0.5, 2.0, size=(s, 7, 2))
+    for q in range(s):
+        for d in range(1, 7):
+            if not (d <= cap and q >= d):
+                y[q, d] = 1.0
+    lds = {}
+    for q in range(rows):
+        for m in range(16):
+            a = y[q, 0, (m >> 3) & 1] * y[q, 1, (m >> 2) & 1] * y[q, 2, (m >> 1) & 1] * y[q, 3, m & 1] if q < s else 0.0
+            b = y[q, 4, (m >> 2) & 1] * y[q, 5, (m >> 1) & 1] * y[q, 6, m & 1] if q < s else 0.0
+            lds[128 * q + 8 * m], lds[kb0 + 128 * q + 8 * m] = a, b
+    for e in range(64):
+        r = [0] * (2 * nb)
+        for q in range(s):
+            if bits[perm[q], e]:
+                r[q >> 5] |= 1 << (q & 31)
+        tot, ap, rp, rc = 0.0, [(-4096) & mask] * 3, 0, r[0]
+        for g in range(2 * nb):
+            av = [0] * 32
+            for t in range(32):
+                x = (rc >> (t - 6)) if t >= 6 else ((((rc << 32) | rp) >> (t + 26)) & mask)
+                av[t] = (x & 0x78) | ((g << 12) & ~0x78 & mask)
+                aq3 = av[t - 3] if t >= 3 else ap[t]
+                tot += lds[(av[t] + 128 * t) & mask] * lds[(aq3 + kb0 + 128 * (t - 3 if t >= 3 else t + 29) + 384) & mask]
+            ap, rp, r = av[29:], rc, r[1:] + [0]
+            rc = r[0]
+        direct = 0.0
+        for q in range(s):
+            v = y[q, 0, bits[perm[q], e]]
+            for d in range(1, 7):
+                v *= y[q, d, bits[perm[q - d], e] if q >= d else 0]
+            direct += v
+        assert abs(tot - direct) <= 1e-12 * abs(direct)
