@@ -118,9 +118,10 @@ def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, w
 
 def c5_capped(torch, dist, stream, batch=2048, steps=10):
     """BASELINE config C5 (S=128, E=5000, parent cap 6): evals/s of the capped
-    lookup-table kernel (fact_kernel 9, what auto takes for capped calls) and
-    of the fp64 MFMA factored kernel (fact_kernel 1) on the same resident
-    inputs; kernel time per launch from the library's HIP events."""
+    lookup-table kernel (fact_kernel 9, what auto takes for capped calls), of
+    its round-1 form (fact_kernel 15) and of the fp64 MFMA factored kernel
+    (fact_kernel 1) on the same resident inputs; kernel time per launch from
+    the library's HIP events."""
     from scipy.special import expit
 
     from nemo import generator
@@ -136,15 +137,31 @@ def c5_capped(torch, dist, stream, batch=2048, steps=10):
     out = {"workload": f"C5: S={S} E={E} cap={cap} {dtype} tables, {batch} evaluations per launch",
            "lookup_table_staged": staged}
     lls = {}
-    for name, fk in ((("lookup_table_kernel", 9),) if staged else ()) + (("f64_mfma_factored_kernel", 1),):
+    runs = ((("lookup_table_kernel", 9), ("lookup_table_kernel_r1", 15)) if staged else ()) + \
+        (("f64_mfma_factored_kernel", 1),)
+    for name, fk in runs:
         eng.set_option("fact_kernel", fk)
         wall, kms = timed_steps(eng, torch, batch, cap, steps, 2, d_pos, d_w01, d_ll, stream, 1, dist)
         lls[name] = d_ll.cpu().numpy()
         out[name] = {"evals_per_s": batch * steps / wall, "kernel_avg_ms": kms,
                      "cells_per_s": batch * S * E / (kms / 1e3)}
     if staged:
+        out["lookup_table_kernel"]["kernel"] = (
+            "score_window2_kernel (row bits transposed into registers, 7-bit window per row by one "
+            "funnel shift; two table reads + one FMA per cell)")
+        out["lookup_table_kernel_r1"]["kernel"] = "score_window_kernel (round 1: row bits re-read from LDS)"
+        # the walk reads two f64 table entries per cell from LDS: priced
+        # against the chip's ds_read_b64 rate (MI355X_MICROARCH.md, LDS table:
+        # 256 B/clk/CU, ~150 TB/s with every CU streaming)
+        kms = out["lookup_table_kernel"]["kernel_avg_ms"]
+        lds_tbs = batch * S * E * 16 / (kms / 1e3) / 1e12
+        out["lookup_table_kernel"]["roofline"] = {
+            "bound": "lds", "achieved": lds_tbs, "peak": 150.0, "unit": "TB/s", "frac": lds_tbs / 150.0,
+            "bytes_per_eval": S * E * 16, "note": "2 x 8 B of LDS reads per cell (S*E cells per evaluation)"}
         out["max_abs_ll_diff"] = float(np.max(np.abs(lls["lookup_table_kernel"] -
                                                      lls["f64_mfma_factored_kernel"])))
+        out["max_abs_ll_diff_r1"] = float(np.max(np.abs(lls["lookup_table_kernel"] -
+                                                        lls["lookup_table_kernel_r1"])))
     eng.close()
     return out
 

@@ -175,7 +175,7 @@ constexpr int kWin2Row = 256;  // bytes of tables per row: A[16] and B'[16], in 
 
 __host__ __device__ __forceinline__ size_t win2_lds_bytes(int S) {
   const int rows = 64 * ((S + 63) / 64);
-  return (size_t)rows * kWin2Row + 64 + 128 * 16 + (size_t)S * 4;
+  return (size_t)rows * kWin2Row + 64 + 128 * 16 + (size_t)S * 7 * 16 + (size_t)S * 4;
 }
 
 __device__ __forceinline__ double lds_f64(uint32_t addr) {
@@ -216,7 +216,8 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
   extern __shared__ __attribute__((aligned(16))) double ldsw[];
   double* lut = ldsw;                                  // at LDS address 0: [ROWS][A 16 | B' 16]
   double2* ltab = (double2*)(ldsw + (size_t)ROWS * 32 + 8);  // log_fast's table
-  int* perm = (int*)(ltab + 128);                      // [S] node at each order position
+  double2* ysc = ltab + 128;                                 // [S][7] factors (table build)
+  int* perm = (int*)(ysc + 7 * S);                           // [S] node at each order position
 
   const int b = blockIdx.x / split;
   const int part = blockIdx.x - b * split;
@@ -236,38 +237,38 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
     perm[p] = i;
   }
   __syncthreads();
-  // one thread per row: y[d][bit] = 1 - w + w e^{T} of parent q-d (d = 1..6;
-  // 1 past the cap / the order start), y[0][bit] = e^{U'} of the row's own bit
+  // the factors of every row: y[q][d] = (1 - w + w e^{lo}, 1 - w + w e^{hi})
+  // of parent q-d (d = 1..6; (1, 1) past the cap / the order start), y[q][0]
+  // = e^{U'} at the row's own bit 0 / 1; one thread per (row, d)
   const double* wb = w01 + (size_t)b * S * S;
-  for (int q = tid; q < ROWS; q += nt) {
-    double* a = lut + (size_t)q * 16;            // A rows at 128 q
-    double* bq = lut + (size_t)kB0 / 8 + (size_t)q * 16;  // B' rows at kB0 + 128 q
-    if (q >= S) {  // padding rows: A = 0 adds nothing
-#pragma unroll
-      for (int m = 0; m < 16; ++m) a[m] = bq[m] = 0.0;
-      continue;
-    }
+  for (int k = tid; k < 7 * S; k += nt) {
+    const int q = k / 7, d = k - 7 * q;
     const int i = perm[q];
-    double y[7][2];
-    y[0][0] = exp(uw[2 * i]);
-    y[0][1] = exp(uw[2 * i + 1]);
-#pragma unroll
-    for (int d = 1; d <= 6; ++d) {
-      y[d][0] = 1.0;
-      y[d][1] = 1.0;
-      if (d <= cap && q >= d) {
-        const int j = perm[q - d];
-        const double s = wb[(size_t)i * S + j];
-        y[d][0] = fma(s, e_lo[j] - 1.0, 1.0);
-        y[d][1] = fma(s, e_hi[j] - 1.0, 1.0);
-      }
+    double2 f = double2{1.0, 1.0};
+    if (d == 0) {
+      f = double2{exp(uw[2 * i]), exp(uw[2 * i + 1])};
+    } else if (d <= cap && q >= d) {
+      const int j = perm[q - d];
+      const double sw = wb[(size_t)i * S + j];
+      f = double2{fma(sw, e_lo[j] - 1.0, 1.0), fma(sw, e_hi[j] - 1.0, 1.0)};
     }
-    // A index bits 0..3 = rows q-3, q-2, q-1, q; B' index bits 0..2 = rows q-6, q-5, q-4
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      a[m] = ((y[0][(m >> 3) & 1] * y[1][(m >> 2) & 1]) * y[2][(m >> 1) & 1]) * y[3][m & 1];
-      bq[m] = (y[4][(m >> 2) & 1] * y[5][(m >> 1) & 1]) * y[6][m & 1];
+    ysc[k] = f;
+  }
+  __syncthreads();
+  // the tables, one thread per entry (consecutive lanes, consecutive entries):
+  // A index bits 0..3 = rows q-3, q-2, q-1, q; B' index bits 0..2 = rows
+  // q-6, q-5, q-4 (bit 3 ignored); padding rows 0 (A = 0 adds nothing)
+  for (int k = tid; k < 32 * ROWS; k += nt) {
+    const int q = k >> 5, m = k & 15;
+    const bool isb = (k & 16) != 0;
+    double v = 0.0;
+    if (q < S) {
+      const double2* y = ysc + 7 * q;
+      auto pick = [&](int d, int bit) { return bit ? y[d].y : y[d].x; };
+      v = isb ? (pick(4, (m >> 2) & 1) * pick(5, (m >> 1) & 1)) * pick(6, m & 1)
+              : ((pick(0, (m >> 3) & 1) * pick(1, (m >> 2) & 1)) * pick(2, (m >> 1) & 1)) * pick(3, m & 1);
     }
+    lut[(isb ? kB0 / 8 : 0) + 16 * q + m] = v;
   }
   __syncthreads();
 
@@ -365,7 +366,13 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
 template <int NB>
 hipError_t launch_window2_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                             double* d_ll, hipStream_t st, int split) {
-  score_window2_kernel<NB, kWinWaves><<<dim3(batch * split), kWinWaves * kWave, win2_lds_bytes(c.S), st>>>(
+  const size_t lds = win2_lds_bytes(c.S);
+  if (lds > 65536) {  // S > 128: past the default 64 KB of dynamic LDS (gfx950 has 160 KB)
+    hipError_t ae = hipFuncSetAttribute((const void*)score_window2_kernel<NB, kWinWaves>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ae != hipSuccess) return ae;
+  }
+  score_window2_kernel<NB, kWinWaves><<<dim3(batch * split), kWinWaves * kWave, lds, st>>>(
       c.S, c.E, c.nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
       c.d_fpartial, d_ll);
   return hipGetLastError();

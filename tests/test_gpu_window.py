@@ -23,7 +23,7 @@ def _pos(perm):
 
 
 @pytest.mark.parametrize("s,e,cap", [(3, 1, 1), (5, 130, 3), (11, 184, 6), (16, 500, 2), (40, 333, 6),
-                                     (64, 2000, 6), (128, 700, 6), (150, 65, 5)])
+                                     (64, 2000, 6), (128, 700, 6), (150, 65, 5), (256, 130, 6)])
 def test_window_kernel_vs_stream_and_oracle(s, e, cap):
     """fact_kernel 9 (and auto, which takes it for ll-only capped calls):
     orders whose first positions have fewer than cap parents, ragged last
