@@ -175,7 +175,7 @@ constexpr int kWin2Row = 256;  // bytes of tables per row: A[16] and B'[16], in 
 
 __host__ __device__ __forceinline__ size_t win2_lds_bytes(int S) {
   const int rows = 64 * ((S + 63) / 64);
-  return (size_t)rows * kWin2Row + 64 + 128 * 16 + (size_t)S * 7 * 16 + (size_t)S * 4;
+  return (size_t)rows * kWin2Row + 64 + 128 * 16 + (size_t)S * 4;
 }
 
 __device__ __forceinline__ double lds_f64(uint32_t addr) {
@@ -216,8 +216,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
   extern __shared__ __attribute__((aligned(16))) double ldsw[];
   double* lut = ldsw;                                  // at LDS address 0: [ROWS][A 16 | B' 16]
   double2* ltab = (double2*)(ldsw + (size_t)ROWS * 32 + 8);  // log_fast's table
-  double2* ysc = ltab + 128;                                 // [S][7] factors (table build)
-  int* perm = (int*)(ysc + 7 * S);                           // [S] node at each order position
+  int* perm = (int*)(ltab + 128);                            // [S] node at each order position
 
   const int b = blockIdx.x / split;
   const int part = blockIdx.x - b * split;
@@ -239,7 +238,9 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
   __syncthreads();
   // the factors of every row: y[q][d] = (1 - w + w e^{lo}, 1 - w + w e^{hi})
   // of parent q-d (d = 1..6; (1, 1) past the cap / the order start), y[q][0]
-  // = e^{U'} at the row's own bit 0 / 1; one thread per (row, d)
+  // = e^{U'} at the row's own bit 0 / 1; one thread per (row, d).  They are
+  // staged in row q's B' slot (112 of its 128 bytes), which is written last.
+  double2* ysc = (double2*)(lut + kB0 / 8);
   const double* wb = w01 + (size_t)b * S * S;
   for (int k = tid; k < 7 * S; k += nt) {
     const int q = k / 7, d = k - 7 * q;
@@ -252,23 +253,35 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
       const double sw = wb[(size_t)i * S + j];
       f = double2{fma(sw, e_lo[j] - 1.0, 1.0), fma(sw, e_hi[j] - 1.0, 1.0)};
     }
-    ysc[k] = f;
+    ysc[8 * q + d] = f;
   }
   __syncthreads();
   // the tables, one thread per entry (consecutive lanes, consecutive entries):
   // A index bits 0..3 = rows q-3, q-2, q-1, q; B' index bits 0..2 = rows
-  // q-6, q-5, q-4 (bit 3 ignored); padding rows 0 (A = 0 adds nothing)
-  for (int k = tid; k < 32 * ROWS; k += nt) {
+  // q-6, q-5, q-4 (bit 3 ignored); padding rows 0 (A = 0 adds nothing).  The
+  // B' entries wait in registers until every thread has read its factors.
+  constexpr int kEpt = 32 * ROWS / (WAVES * kWave);  // entries per thread
+  double bv[kEpt];
+#pragma unroll
+  for (int e = 0; e < kEpt; ++e) {
+    const int k = tid + e * WAVES * kWave;
     const int q = k >> 5, m = k & 15;
     const bool isb = (k & 16) != 0;
     double v = 0.0;
     if (q < S) {
-      const double2* y = ysc + 7 * q;
+      const double2* y = ysc + 8 * q;
       auto pick = [&](int d, int bit) { return bit ? y[d].y : y[d].x; };
       v = isb ? (pick(4, (m >> 2) & 1) * pick(5, (m >> 1) & 1)) * pick(6, m & 1)
               : ((pick(0, (m >> 3) & 1) * pick(1, (m >> 2) & 1)) * pick(2, (m >> 1) & 1)) * pick(3, m & 1);
     }
-    lut[(isb ? kB0 / 8 : 0) + 16 * q + m] = v;
+    if (!isb) lut[16 * q + m] = v;
+    bv[e] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kEpt; ++e) {
+    const int k = tid + e * WAVES * kWave;
+    if (k & 16) lut[kB0 / 8 + 16 * (k >> 5) + (k & 15)] = bv[e];
   }
   __syncthreads();
 
