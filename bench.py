@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F64_MFMA_PEAK_TF = 78.6  # v_mfma_f64_16x16x4_f64: 2048 FLOP / 64 busy cycles / SIMD (PMC-checked)
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (MI355X_MICROARCH.md: 2x the ~2.5 PF BF16 rate)
 PATHS = {"auto": 0, "stream": 1, "factored": 2}
 
 
@@ -308,6 +309,15 @@ def main():
                             "(S*E exps/eval) beside the MFMAs: valu_bound (PMC, profiles/valu.json; "
                             "DESIGN.md 3.1e)",
                     "valu_bound": load_valu_bound(f"{args.config}:{tkey}:b{B}")}
+            if i8l:
+                # what the matrix cores actually execute: 7 v_mfma_i32_16x16x64_i8
+                # (2*16*16*64 ops each) per 16-child row block per 16-effect tile,
+                # against the dense int8 peak (2x BF16 per clock, ~5 POPS)
+                ops = ((E + 15) // 16) * (4 if S > 32 else 2 if S > 16 else 1) * 7 * 32768
+                roof["int8_mfma_executed"] = {
+                    "achieved": B * ops / (kern_ms / 1e3) / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                    "frac": B * ops / (kern_ms / 1e3) / 1e12 / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops,
+                    "note": "the matrix pipe is ~27% busy (PMC mfma_busy); the epilogue's VALU issue binds"}
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
             ach = B * bpe / (kern_ms / 1e3) / 1e9
