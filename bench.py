@@ -281,12 +281,13 @@ def main():
             fpe = algorithmic_flops_per_eval(S, E, cap)
             ach = B * fpe / (kern_ms / 1e3) / 1e12
             fk = eng.get_option("fact_kernel")
-            i8l = S <= 64 and eng.get_option("i8l") > 0 and fk in (0, 10, 11, 12, 13)
+            i8l = S <= 64 and eng.get_option("i8l") > 0 and fk in (0, 10, 11, 12, 13, 14, 16)
             i8o = not i8l and S <= 64 and eng.get_option("i8o") > 0 and fk in (0, 7, 8)
             i8 = S <= 64 and (i8l or i8o or fk in (4, 5, 6))
             kname = ("score_i8l_kernel (x / ln 2 = Delta.D1 + U' + G exact in int8 fixed point on "
                      "v_mfma_i32_16x16x64_i8, 7 digit slices; e^x assembled from the integer "
-                     "accumulators + table + degree-2 series; log-sum-exp offset by the null row)"
+                     "accumulators + table + degree-2 series; log-sum-exp offset by the null row; "
+                     "two 16-effect tiles per iteration share the A fragments)"
                      if i8l else
                      "score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on "
                      "v_mfma_i32_16x16x64_i8, fp64 cells, log-sum-exp offset by the null row)" if i8o else

@@ -180,9 +180,12 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                calls when the model passes its checks (option "win");
  *                10 / 11 = the offset kernel in log2 fixed point (8 / 4
  *                waves), which auto prefers over 7 / 8 when staged
- *                (option "i8l"); 12 = the same with 16 waves per block,
- *                13 = its register-stationary variant, 14 = 8 waves
- *                compiled for 6 waves per SIMD (same bits as 10);
+ *                (option "i8l"; 10 walks two 16-effect tiles per
+ *                iteration); 12 = the same with 16 waves per block,
+ *                13 = its register-stationary variant, 14 = 8 waves with
+ *                one tile per iteration compiled for 6 waves per SIMD,
+ *                16 = 8 waves with one tile per iteration (14 and 16 give
+ *                10's bits);
  *                15 = the round-1 form of 9 (row bits re-read from LDS)
  *   "factored"   (get only) 1 if the staged table is factorable
  *   "win"        (get only) 1 if the capped lookup-table kernel is staged

@@ -948,7 +948,7 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
 // units 2^-38): 7 MFMAs per row block against 8.  Requires the diagonal form
 // (stage_i8o).
 // ---------------------------------------------------------------------------
-template <int NR, int WAVES, int OCC>
+template <int NR, int WAVES, int OCC, int TT = 1>
 __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
@@ -1027,83 +1027,174 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
   const i32x4* Gi = (const i32x4*)gi;
   const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
   int set = s_begin + w;
-  if (set < s_end) {
-    double lprod = 1.0;
-    int lexp = 0;
-    int t = 8 * set;
-    i32x4 bc = Bt[(size_t)t * kWave + lane];
-    i32x4 bc64 = Bt64[(size_t)t * kWave + lane];
-    for (;;) {
-      uint32_t ao = a_lane;
-      asm volatile("" : "+v"(ao));
-      const i32x4* Al = ev.A + ao;
-      int tn = t + 1, setn = set;
-      if (tn >= min(ntiles, 8 * set + 8)) {
-        setn = set + WAVES;
-        tn = 8 * setn;
-      }
-      const bool more = setn < s_end;
-      const int tl = more ? tn : t;  // prefetch target (the current tile again at the end)
-      const i32x4 b1 = bc, b64 = bc64;
-      bc = Bt[(size_t)tl * kWave + lane];
-      bc64 = Bt64[(size_t)tl * kWave + lane];
-      double ls0 = 0.0, ls1 = 0.0;
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const i32x4 c0 = Gi[(16 * r) / 4 + rg];
-        const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
-#if NEMO_I8_ABLATE & 128  // instrumented build: half the A-fragment reads (wrong values)
-        auto A = [&](int sl) { return Al[((sl & ~1) * SPAD + 16 * r) * 4]; };
-#else
-        auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
-#endif
-#if NEMO_I8_ABLATE & 2  // instrumented build: no MFMA (one add per pair; wrong values)
-        const i32x4 h0 = A(0) + A(1) + b64, h1 = A(2) + A(3) + c0, l0 = A(4) + b1,
-                    l1 = A(5) + A(6) + c1;
-#else
-        i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0), b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1), b1, h0, 0, 0, 0);
-        i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2), b64, c0, 0, 0, 0);
-        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3), b1, h1, 0, 0, 0);
-        const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4), b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
-        i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5), b64, c1, 0, 0, 0);
-        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6), b1, l1, 0, 0, 0);
-#endif
-        // the row block's 4 cells per lane in three phases, so the 4 table
-        // reads (random entries: ~3.5-way bank conflicts) are in flight
-        // while the series runs: addresses + reads, series, then assembly
-        uint32_t t0[4];
-        uint64_t ev[4];
-        double pr[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          // T_0 wraps mod 2^32 only transiently (its true value is in (0, 2^31))
-          t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
-          ev[g] = exp2_fx_load(t0[g]);
+  if constexpr (TT == 1) {
+    int set = s_begin + w;
+    if (set < s_end) {
+      double lprod = 1.0;
+      int lexp = 0;
+      int t = 8 * set;
+      i32x4 bc = Bt[(size_t)t * kWave + lane];
+      i32x4 bc64 = Bt64[(size_t)t * kWave + lane];
+      for (;;) {
+        uint32_t ao = a_lane;
+        asm volatile("" : "+v"(ao));
+        const i32x4* Al = ev.A + ao;
+        int tn = t + 1, setn = set;
+        if (tn >= min(ntiles, 8 * set + 8)) {
+          setn = set + WAVES;
+          tn = 8 * setn;
         }
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if (g & 1) ls1 = exp2_fx_apply(t0[g], ev[g], pr[g], ls1);
-          else ls0 = exp2_fx_apply(t0[g], ev[g], pr[g], ls0);
+        const bool more = setn < s_end;
+        const int tl = more ? tn : t;  // prefetch target (the current tile again at the end)
+        const i32x4 b1 = bc, b64 = bc64;
+        bc = Bt[(size_t)tl * kWave + lane];
+        bc64 = Bt64[(size_t)tl * kWave + lane];
+        double ls0 = 0.0, ls1 = 0.0;
+  #pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+          const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+  #if NEMO_I8_ABLATE & 128  // instrumented build: half the A-fragment reads (wrong values)
+          auto A = [&](int sl) { return Al[((sl & ~1) * SPAD + 16 * r) * 4]; };
+  #else
+          auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
+  #endif
+  #if NEMO_I8_ABLATE & 2  // instrumented build: no MFMA (one add per pair; wrong values)
+          const i32x4 h0 = A(0) + A(1) + b64, h1 = A(2) + A(3) + c0, l0 = A(4) + b1,
+                      l1 = A(5) + A(6) + c1;
+  #else
+          i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0), b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1), b1, h0, 0, 0, 0);
+          i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2), b64, c0, 0, 0, 0);
+          h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3), b1, h1, 0, 0, 0);
+          const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4), b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5), b64, c1, 0, 0, 0);
+          l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6), b1, l1, 0, 0, 0);
+  #endif
+          // the row block's 4 cells per lane in three phases, so the 4 table
+          // reads (random entries: ~3.5-way bank conflicts) are in flight
+          // while the series runs: addresses + reads, series, then assembly
+          uint32_t t0[4];
+          uint64_t ev[4];
+          double pr[4];
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            // T_0 wraps mod 2^32 only transiently (its true value is in (0, 2^31))
+            t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+            ev[g] = exp2_fx_load(t0[g]);
+          }
+  #pragma unroll
+          for (int g = 0; g < 4; ++g)
+            pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g & 1) ls1 = exp2_fx_apply(t0[g], ev[g], pr[g], ls1);
+            else ls0 = exp2_fx_apply(t0[g], ev[g], pr[g], ls0);
+          }
         }
+        double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
+        lprod *= t * 16 + col < E ? l : 1.0;
+        lexp += __builtin_amdgcn_frexp_exp(lprod);
+        lprod = __builtin_amdgcn_frexp_mant(lprod);
+        if (setn != set) {  // set complete: one partial
+          double v = log(lprod) + (double)lexp * 0.69314718055994530942;
+          v = wsum(lane < 16 ? v : 0.0);
+          if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+          lprod = 1.0;
+          lexp = 0;
+        }
+        if (!more) break;
+        t = tn;
+        set = setn;
       }
-      double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
-      lprod *= t * 16 + col < E ? l : 1.0;
-      lexp += __builtin_amdgcn_frexp_exp(lprod);
-      lprod = __builtin_amdgcn_frexp_mant(lprod);
-      if (setn != set) {  // set complete: one partial
-        double v = log(lprod) + (double)lexp * 0.69314718055994530942;
-        v = wsum(lane < 16 ? v : 0.0);
-        if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
-        lprod = 1.0;
-        lexp = 0;
+    }
+  } else {
+    // TT = 2: two 16-effect tiles per iteration share each row block's A
+    // fragments and G C-inits (half the A-fragment LDS reads); the same
+    // arithmetic per cell and the same order of the column products as TT = 1,
+    // so the same bits.  The second tile of a set's odd tail repeats the first
+    // and is not multiplied in.
+    if (set < s_end) {
+      double lprod = 1.0;
+      int lexp = 0;
+      int t = 8 * set;
+      auto tend = [&](int st) { return min(ntiles, 8 * st + 8); };
+      int t2 = t + 1 < tend(set) ? t + 1 : t;
+      i32x4 bca = Bt[(size_t)t * kWave + lane], bca64 = Bt64[(size_t)t * kWave + lane];
+      i32x4 bcb = Bt[(size_t)t2 * kWave + lane], bcb64 = Bt64[(size_t)t2 * kWave + lane];
+      for (;;) {
+        uint32_t ao = a_lane;
+        asm volatile("" : "+v"(ao));
+        const i32x4* Al = ev.A + ao;
+        const bool two = t2 != t;
+        int tn = t + 2, setn = set;
+        if (tn >= tend(set)) {
+          setn = set + WAVES;
+          tn = 8 * setn;
+        }
+        const bool more = setn < s_end;
+        const int tla = more ? tn : t;
+        const int tlb = more ? (tn + 1 < tend(setn) ? tn + 1 : tn) : t;
+        const i32x4 b1a = bca, b64a = bca64, b1b = bcb, b64b = bcb64;
+        bca = Bt[(size_t)tla * kWave + lane];
+        bca64 = Bt64[(size_t)tla * kWave + lane];
+        bcb = Bt[(size_t)tlb * kWave + lane];
+        bcb64 = Bt64[(size_t)tlb * kWave + lane];
+        double la0 = 0.0, la1 = 0.0, lb0 = 0.0, lb1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+          const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+          auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
+          const i32x4 a0 = A(0), a1 = A(1), a2 = A(2), a3 = A(3), a4 = A(4), a5 = A(5), a6 = A(6);
+          auto tile = [&](const i32x4 b1, const i32x4 b64, double& ls0, double& ls1) {
+            i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, h0, 0, 0, 0);
+            i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, b64, c0, 0, 0, 0);
+            h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a3, b1, h1, 0, 0, 0);
+            const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a5, b64, c1, 0, 0, 0);
+            l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a6, b1, l1, 0, 0, 0);
+            uint32_t t0[4];
+            uint64_t evv[4];
+            double pr[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+              evv[g] = exp2_fx_load(t0[g]);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+              else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+            }
+          };
+          tile(b1a, b64a, la0, la1);
+          tile(b1b, b64b, lb0, lb1);
+        }
+        double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
+        lprod *= t * 16 + col < E ? l : 1.0;
+        lexp += __builtin_amdgcn_frexp_exp(lprod);
+        lprod = __builtin_amdgcn_frexp_mant(lprod);
+        l = rowsum4(lb0 + lb1) + 1.0;
+        lprod *= two && t2 * 16 + col < E ? l : 1.0;
+        lexp += __builtin_amdgcn_frexp_exp(lprod);
+        lprod = __builtin_amdgcn_frexp_mant(lprod);
+        if (setn != set) {  // set complete: one partial
+          double v = log(lprod) + (double)lexp * 0.69314718055994530942;
+          v = wsum(lane < 16 ? v : 0.0);
+          if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+          lprod = 1.0;
+          lexp = 0;
+        }
+        if (!more) break;
+        t = tn;
+        t2 = tlb;
+        set = setn;
       }
-      if (!more) break;
-      t = tn;
-      set = setn;
     }
   }
   if (split == 1) {
@@ -1307,7 +1398,7 @@ hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   return hipGetLastError();
 }
 
-template <int NR, int WAVES, int OCC = NEMO_I8O_WAVES_PER_SIMD>
+template <int NR, int WAVES, int OCC = NEMO_I8O_WAVES_PER_SIMD, int TT = 1>
 hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
@@ -1317,7 +1408,7 @@ hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   int split = (slots + batch - 1) / batch;
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)7 * SPAD * 64;
-  score_i8l_kernel<NR, WAVES, OCC><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+  score_i8l_kernel<NR, WAVES, OCC, TT><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
       c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
@@ -1340,6 +1431,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
            : waves == 16 ? launch_i8l_t<NRV, 16>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
            : waves == -8 ? launch_i8l_t<NRV, 8, 6>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == -2 ? launch_i8l_t<NRV, 8, 4, 2>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                          : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \

@@ -347,7 +347,7 @@ def test_factored_kernel_variants_agree(s, e):
         assert eng.get_option("i8o") == (2 if s <= 64 else 0)
         assert eng.get_option("i8l") == (1 if s <= 64 else 0)
         for fk, nodiag in ((1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (6, 0), (7, 0), (8, 0), (7, 1), (8, 1),
-                           (10, 0), (11, 0), (12, 0), (13, 0)):
+                           (10, 0), (11, 0), (12, 0), (13, 0), (14, 0), (16, 0)):
             eng.set_option("fact_kernel", fk)
             eng.set_option("i8o_nodiag", nodiag)
             ll = eng.score(pos, w01, cap=cap)
@@ -414,11 +414,12 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
-    # auto is the log2 fixed-point offset kernel; its 8 and 4 waves per block
-    # give the same bits, and so do the natural-scale offset kernel's (7 / 8)
-    # and the max-offset kernel's (4 / 6)
+    # auto is the log2 fixed-point offset kernel; its 8 and 4 waves per block,
+    # one or two effect tiles per iteration and 6 waves per SIMD give the same
+    # bits, and so do the natural-scale offset kernel's (7 / 8) and the
+    # max-offset kernel's (4 / 6)
     assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
-    for fk in (10, 11, 12):
+    for fk in (10, 11, 12, 14, 16):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
