@@ -665,8 +665,8 @@ hipError_t launch_i8_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const d
 // 1.5 2^52 + kBias, kBias = 1023 * 2048, so the low dword of t is k + kBias
 // (> 0 for x > -709): its low 11 bits are the table index j = k & 2047 and
 // (lo << 9) = ((k >> 11) + 1023) << 20 + (j << 9).  The table entry's high
-// dword is stored as hi(2^(j/2048)) with its exponent field cleared, minus
-// (j << 9), so one shift-add makes the exponent field 1023 + (k >> 11) (no
+// dword is stored as hi(2^(j/2048)) with its exponent field cleared, XOR
+// (j << 9), so one shift-xor makes the exponent field 1023 + (k >> 11) (no
 // ldexp; |x| <= 700 keeps it normal).  Table: kExpTabN entries, 16 KB.
 constexpr int kExpTabN = 2048;
 constexpr double kExpMagicB = 6755399441055744.0 + 1023.0 * 2048.0;
@@ -686,15 +686,15 @@ __device__ __forceinline__ double exp_acc(double x, const uint2* __restrict__ ta
 #else
   const uint2 e = tab[lo & (kExpTabN - 1)];
 #endif
-  const uint32_t hi = (lo << 9) + e.y;
+  const uint32_t hi = (lo << 9) ^ e.y;
   return fma(p, __builtin_bit_cast(double, ((uint64_t)hi << 32) | e.x), acc);
 }
 
 // acc + 2^y for score_i8l_kernel, y = (T_0 2^-20 + T_1 2^-38) - 1023: T_0
 // carries the exponent bias (G's C-init), so bits 20..30 of T_0 are the
 // biased exponent 1023 + floor(y) and bits 9..19 the index j of 2^(j/2048).
-// The table's high dword is stored with its exponent field cleared, minus
-// (j << 9) (exp_acc's table), so (T_0 & ~511) + e.y is the high dword of
+// The table's high dword is stored with its exponent field cleared, XOR
+// (j << 9) (exp_acc's table), so (T_0 & ~511) ^ e.y is the high dword of
 // 2^(floor(y) + j/2048): no range reduction in f64.  The remainder
 // R = (T_0 & 511) 2^18 + T_1 (units of 2^-38, |R| < 2^28: one shift-add and
 // one conversion, exact) gives f = R 2^-38 ln 2 in (-2.2e-5, 3.6e-4), where
@@ -721,11 +721,16 @@ __device__ __forceinline__ uint64_t exp2_fx_load(uint32_t t0) {
   return *(const __attribute__((address_space(3))) uint64_t*)(size_t)addr;
 }
 __device__ __forceinline__ double exp2_fx_series(uint32_t t0, int t1) {
-  const double r = (double)(int)(((t0 & 511u) << 18) + (uint32_t)t1);
+  // R = (T_0 & 511) 2^18 + T_1 as one v_lshl_add_u32 after the mask (the
+  // compiler's own form is two shifts, an AND and an add3)
+  uint32_t rr;
+  asm("v_lshl_add_u32 %0, %1, 18, %2" : "=v"(rr) : "v"(t0 & 511u), "v"((uint32_t)t1));
+  const double r = (double)(int)rr;
   return fma(r, fma(r, kL2C2, kL2C1), kL2C0);
 }
 __device__ __forceinline__ double exp2_fx_apply(uint32_t t0, uint64_t ev, double p, double acc) {
-  const uint32_t hi = (t0 & ~511u) + (uint32_t)(ev >> 32);
+  // (one v_bitop3: bits 9-19 of T_0 cancel the index the entry carries)
+  const uint32_t hi = (t0 & ~511u) ^ (uint32_t)(ev >> 32);
   return fma(__builtin_bit_cast(double, ((uint64_t)hi << 32) | (uint32_t)ev), p, acc);
 }
 
@@ -1507,7 +1512,7 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       uint64_t b;
       memcpy(&b, &v, 8);
       tb[2 * j] = (uint32_t)b;
-      tb[2 * j + 1] = ((uint32_t)(b >> 32) & 0x800fffffu) - ((uint32_t)j << 9);
+      tb[2 * j + 1] = ((uint32_t)(b >> 32) & 0x800fffffu) ^ ((uint32_t)j << 9);
     }
     double* lt = (double*)(tb.data() + kExpTabN * 2);
     for (int k = 0; k < 128; ++k) {

@@ -139,7 +139,7 @@ def _l2_table():
     for j in range(2048):
         v = float(mpmath.mpf(2) ** (mpmath.mpf(j) / 2048))
         b = int(np.float64(v).view(np.uint64))
-        tab.append((b & 0xFFFFFFFF, (((b >> 32) & 0x800FFFFF) - (j << 9)) & 0xFFFFFFFF))
+        tab.append((b & 0xFFFFFFFF, ((b >> 32) & 0x800FFFFF) ^ (j << 9)))
     return tab
 
 
@@ -148,7 +148,7 @@ def exp2_fx(t0, t1, tab):
     t0 &= 0xFFFFFFFF
     low = t0 & 511
     lo, hi_t = tab[(t0 >> 6 & 0x3FF8) >> 3]
-    hi = ((t0 & ~511 & 0xFFFFFFFF) + hi_t) & 0xFFFFFFFF
+    hi = (t0 & ~511 & 0xFFFFFFFF) ^ hi_t
     value = float(np.uint64((hi << 32) | lo).view(np.float64))
     r32 = ((low << 18) + t1) & 0xFFFFFFFF
     r = float(r32 - (1 << 32) if r32 >= 1 << 31 else r32)
