@@ -13,17 +13,24 @@ import sys
 
 
 def per_kernel(path, counter):
-    agg = collections.defaultdict(list)
+    """Mean per dispatch (rows of one dispatch summed), the first (cold)
+    dispatch of each kernel dropped when there are others."""
+    per = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        for tag, kind in (("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+        for tag, kind in (("score_window2_kernel", "win2"), ("score_window_kernel", "win"),
+                          ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"),
+                          ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
                           ("score_factored_kernel", "factored"), ("score_kernel", "stream")):
             if tag in name:
-                agg[kind].append(float(r["Counter_Value"]))
+                per[(kind, int(r["Dispatch_Id"]))] += float(r["Counter_Value"])
                 break
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+    agg = collections.defaultdict(list)
+    for (kind, disp), v in sorted(per.items()):
+        agg[kind].append(v)
+    return {k: sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0] for k, v in agg.items()}
 
 
 def main():
