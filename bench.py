@@ -70,6 +70,55 @@ def cpu_baseline(m, seconds=10.0):
                       "loop form (reference operation order), one thread, this host"}
 
 
+_CPU_CHILD = r"""
+import sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import nemo_oracle as no
+from scipy.special import expit
+from nemo import generator
+m = generator.config_nem(sys.argv[3]); t = m.get_score_tensor()
+rng = np.random.default_rng(int(sys.argv[5]))
+sys.stdout.write("ready\n"); sys.stdout.flush()
+sys.stdin.readline()
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < float(sys.argv[4]):
+    no.order_score(m.U, t, rng.permutation(m.num_s), expit(rng.uniform(-3, 3, (m.num_s, m.num_s))))
+    n += 1
+print(n, time.perf_counter() - t0)
+"""
+
+
+def cpu_baseline_procs(config, nproc=8, seconds=10.0):
+    """the same oracle loop in nproc independent processes
+    (one thread each, independent chains), started together; the rate is the
+    sum of the processes' own rates.  Children are plain subprocesses that
+    never touch the GPU."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    args = [os.path.join(HERE, "oracle"), os.path.join(HERE, "nem-mcmc-optimization_amd"), config, str(seconds)]
+    procs = [subprocess.Popen([sys.executable, "-c", _CPU_CHILD] + args + [str(100 + k)], stdin=subprocess.PIPE,
+                              stdout=subprocess.PIPE, text=True, env=env) for k in range(nproc)]
+    try:
+        for p in procs:  # every child has built its model before any starts timing
+            if p.stdout.readline().strip() != "ready":
+                raise RuntimeError("cpu baseline child failed to start")
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        res = [p.communicate(timeout=seconds + 120)[0].split() for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    rates = [int(n) / float(dt) for n, dt in res]
+    n = sum(int(r[0]) for r in res)
+    return {"value": sum(rates), "unit": "evals/s", "cores": nproc, "kind": "port",
+            "sample": f"{n} order-score evals of the {config} model by {nproc} independent one-thread "
+                      f"processes in ~{seconds:.0f} s each: oracle numpy loop form (reference operation "
+                      "order), this host"}
+
+
 def load_valu_bound(key):
     """PMC-derived VALU utilisation of the score kernel (profiles/valu.json,
     tools/make_valu.py): VALU-busy cycles over SIMD cycles."""
@@ -178,6 +227,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the stream-kernel and MCMC lines")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=8,
+                    help="processes of the multi-process CPU baseline (1: off)")
     args = ap.parse_args()
 
     import torch
@@ -351,6 +402,8 @@ def main():
         rec.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(m, args.cpu_seconds)
+            if args.cpu_procs > 1:  # also all the host cores the round budget allows
+                rec["cpu_baseline_procs"] = cpu_baseline_procs(args.config, args.cpu_procs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
