@@ -659,6 +659,9 @@ hipError_t launch_i8_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const d
 #ifndef NEMO_I8O_WAVES_PER_SIMD
 #define NEMO_I8O_WAVES_PER_SIMD 4
 #endif
+#ifndef NEMO_I8L2_OCC  // waves per SIMD the two-tile log2 kernel is compiled for
+#define NEMO_I8L2_OCC 4
+#endif
 
 // acc + e^x for |x| <= 700: 2^(k/2048) e^r, k = rint(x 2048/ln2), |r| <=
 // ln2/4096, degree-3 series (error r^4/24 < 4e-17).  The rounding constant is
@@ -1151,15 +1154,45 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
           const i32x4 c0 = Gi[(16 * r) / 4 + rg];
           const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
           auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
-          const i32x4 a0 = A(0), a1 = A(1), a2 = A(2), a3 = A(3), a4 = A(4), a5 = A(5), a6 = A(6);
-          auto tile = [&](const i32x4 b1, const i32x4 b64, double& ls0, double& ls1) {
-            i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b64, i32x4{0, 0, 0, 0}, 0, 0, 0);
-            h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, h0, 0, 0, 0);
-            i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, b64, c0, 0, 0, 0);
-            h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a3, b1, h1, 0, 0, 0);
-            const i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a4, b1, i32x4{0, 0, 0, 0}, 0, 0, 0);
-            i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a5, b64, c1, 0, 0, 0);
-            l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a6, b1, l1, 0, 0, 0);
+          // slice by slice for both tiles: each A fragment dies after its two MFMAs
+          i32x4 h0a, h0b, h1a, h1b, l0a, l0b, l1a, l1b;
+          {
+            const i32x4 a = A(0);
+            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(1);
+            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h0a, 0, 0, 0);
+            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h0b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(2);
+            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c0, 0, 0, 0);
+            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c0, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(3);
+            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h1a, 0, 0, 0);
+            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h1b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(4);
+            l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, i32x4{0, 0, 0, 0}, 0, 0, 0);
+            l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(5);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(6);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
+          }
+          auto epi = [&](const i32x4 h0, const i32x4 h1, const i32x4 l0, const i32x4 l1, double& ls0,
+                         double& ls1) {
             uint32_t t0[4];
             uint64_t evv[4];
             double pr[4];
@@ -1177,8 +1210,8 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
               else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
             }
           };
-          tile(b1a, b64a, la0, la1);
-          tile(b1b, b64b, lb0, lb1);
+          epi(h0a, h1a, l0a, l1a, la0, la1);
+          epi(h0b, h1b, l0b, l1b, lb0, lb1);
         }
         double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
         lprod *= t * 16 + col < E ? l : 1.0;
@@ -1436,7 +1469,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
            : waves == 16 ? launch_i8l_t<NRV, 16>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
            : waves == -8 ? launch_i8l_t<NRV, 8, 6>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
-           : waves == -2 ? launch_i8l_t<NRV, 8, 4, 2>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == -2 ? launch_i8l_t<NRV, 8, NEMO_I8L2_OCC, 2>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                          : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
