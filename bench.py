@@ -369,7 +369,7 @@ def main():
                 roof["int8_mfma_executed"] = {
                     "achieved": B * ops / (kern_ms / 1e3) / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                     "frac": B * ops / (kern_ms / 1e3) / 1e12 / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops,
-                    "note": "the matrix pipe is ~27% busy (PMC mfma_busy); the epilogue's VALU issue binds"}
+                    "note": "the matrix pipe is ~30% busy (PMC mfma_busy, valu_bound); the epilogue VALU issue binds"}
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
             ach = B * bpe / (kern_ms / 1e3) / 1e9
