@@ -59,12 +59,17 @@ def _prepare(chains):
     """Host inputs of ``get_optimal_weights`` for a group of chains: positions,
     weights, expit(weights) and ancestor_x = clip(inv(I - W~) - I, 0, 1) with W~
     the weights under expit on the permissible entries only
-    (nem_order_mcmc.py:98-103, :185)."""
+    (nem_order_mcmc.py:98-103, :185).  W~ doubles as the device's w01: the
+    kernels read it at permissible (child, parent) entries only, where it is
+    expit(W); expit runs on those entries alone (scipy's ufunc is elementwise,
+    so the bits are those of expit over the whole matrix)."""
     s = chains[0].num_s
     pos = np.stack([c._pos for c in chains]).astype(np.int32)
     w = np.stack([c.parent_weights for c in chains])
-    w01 = expit(w)
-    sig = np.where(np.stack([c._mask for c in chains]), w01, w)
+    mask = np.stack([c._mask for c in chains])
+    sig = w.copy()
+    sig[mask] = expit(w[mask])
+    w01 = sig
     eye = np.identity(s)
     anc = np.clip(inv_stack(eye - sig) - eye, 0, 1)
     for k, c in enumerate(chains):
