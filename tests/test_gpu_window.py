@@ -50,6 +50,13 @@ def test_window_kernel_vs_stream_and_oracle(s, e, cap):
         assert abs(ll[c] - no.order_score(m.U, t, perms[c], w01[c], cap=cap)) <= TOL
     eng.set_option("fact_kernel", 0)
     assert np.array_equal(eng.score(pos, w01, cap=cap), ll)
+    # the round-1 form (row bits re-read from LDS, exp of summed logs): its own
+    # bits, the same values
+    eng.set_option("fact_kernel", 15)
+    r1 = eng.score(pos, w01, cap=cap)
+    assert np.max(np.abs(r1 - ll)) <= TOL
+    assert eng.score(pos[5:6], w01[5:6], cap=cap)[0] == r1[5]
+    eng.set_option("fact_kernel", 0)
     # weights at 0 and 1: every factor at its extremes
     for w in (0.0, 1.0):
         wz = np.full((2, s, s), w)
