@@ -418,7 +418,13 @@ hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos,
   const int slots = 768;
   int split = (slots + batch - 1) / batch;
   split = std::max(1, std::min(split, (nwords + kWinWaves - 1) / kWinWaves));
-  score_window_kernel<kWinWaves><<<dim3(batch * split), kWinWaves * kWave, win_lds_bytes(c.S, kWinWaves), st>>>(
+  const size_t lds1 = win_lds_bytes(c.S, kWinWaves);
+  if (lds1 > 65536) {  // past the default 64 KB of dynamic LDS
+    hipError_t ae = hipFuncSetAttribute((const void*)score_window_kernel<kWinWaves>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+    if (ae != hipSuccess) return ae;
+  }
+  score_window_kernel<kWinWaves><<<dim3(batch * split), kWinWaves * kWave, lds1, st>>>(
       c.S, c.E, nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
       c.d_fpartial, d_ll);
   *nparts = nwords;
