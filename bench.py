@@ -154,6 +154,8 @@ def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, w
     if world > 1:
         # C4: gather every rank's per-chain best score (tiny, latency-bound)
         best = d_ll.max().reshape(1)
+        if dist.get_backend() != "nccl":
+            best = best.cpu()
         allb = [torch.empty_like(best) for _ in range(world)]
         dist.all_gather(allb, best)
     torch.cuda.synchronize()
@@ -237,9 +239,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NEMO_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # one GPU (device = local rank modulo the visible GPUs); the driver's
+    # multi-GPU runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("NEMO_BENCH_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1) if backend != "nccl" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from scipy.special import expit
 
@@ -265,7 +275,7 @@ def main():
 
     wall, kern_ms = timed_steps(eng, torch, B, cap, args.steps, args.warmup, d_pos, d_w01, d_ll,
                                 stream, world, dist)
-    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    t_max = torch.tensor([wall], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     t_max = float(t_max.item())
