@@ -157,11 +157,12 @@ __global__ __launch_bounds__(WAVES * kWave) void score_window_kernel(
 // so X_q & 0x78 is directly the byte offset of row q's A entry (own bit and
 // parents 1-3, 16 entries).  Parents 4-6 of row q are rows q-6 .. q-4, the
 // low three bits of row q-3's A index: row q's second table B' is stored with
-// 16 entries (B'[m] = B[m & 7]) and read at row q-3's A offset.  Row q's tables
-// sit at q * 256 bytes (A, then B'), so with the rows unrolled every table
-// offset is an instruction immediate and a cell costs one shift, one AND, two
-// LDS reads and one FMA (against ~9 VALU and three LDS reads in
-// score_window_kernel, which re-extracts each row's bit from an LDS word).
+// 16 entries (B'[m] = B[m & 7]) and read at row q-3's A offset.  Row q's A
+// sits at 128 q, its B' at kB0 + 128 q; the rows run in 32-row groups,
+// unrolled, so every row offset is an instruction immediate and a cell costs
+// one shift, one bit select (group base), two LDS reads and one FMA (against
+// ~9 VALU and three LDS reads in score_window_kernel, which re-extracts each
+// row's bit from an LDS word).
 // Tables are products of the per-parent factors 1 - w + w e^{T} (the terms
 // whose logs the cell sums) and e^{U'}: no log or exp per entry.
 // ---------------------------------------------------------------------------
@@ -169,9 +170,6 @@ constexpr int kWin2Row = 256;  // bytes of tables per row: A[16] and B'[16], in 
 #ifndef NEMO_WIN2_OCC
 #define NEMO_WIN2_OCC 6
 #endif
-#ifndef NEMO_WIN2_CHUNK
-#define NEMO_WIN2_CHUNK 8
-#endif  // bytes of one row's tables (A[16], B'[16])
 
 __host__ __device__ __forceinline__ size_t win2_lds_bytes(int S) {
   const int rows = 64 * ((S + 63) / 64);
@@ -214,7 +212,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
   // 128 B/clk against 256 for two ds_read_b64)
   constexpr int kB0 = ROWS * 128 + 64;
   extern __shared__ __attribute__((aligned(16))) double ldsw[];
-  double* lut = ldsw;                                  // at LDS address 0: [ROWS][A 16 | B' 16]
+  double* lut = ldsw;  // at LDS address 0: A [ROWS][16], then B' [ROWS][16] from kB0
   double2* ltab = (double2*)(ldsw + (size_t)ROWS * 32 + 8);  // log_fast's table
   int* perm = (int*)(ltab + 128);                            // [S] node at each order position
 
