@@ -320,17 +320,25 @@ def main():
         from nemo.chains import ChainBatch
         order0 = nutils.initial_order_guess(m.observed_knockdown_mat)
         seeds = [1234 + c for c in range(nch)]
-        ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue").run(2)
-        cb = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue")
+        from nemo.invpool import InvPool
+        pool = InvPool(S, nch, n_workers=4)
         n_it = 20
-        t0 = time.perf_counter()
-        cb.run(n_it)
-        dt = time.perf_counter() - t0
+        e2e = {}
+        for tag, pl in (("pool", pool), ("serial", None)):
+            ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pl).run(2)
+            cb = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pl)
+            t0 = time.perf_counter()
+            cb.run(n_it)
+            e2e[tag] = (time.perf_counter() - t0, cb.best_scores)
+        pool.close()
+        dt = e2e["pool"][0]
         extras["mcmc_end_to_end"] = {
             "chains": nch, "steps": n_it, "ms_per_step": 1e3 * dt / n_it,
             "chain_steps_per_s": nch * n_it / dt,
-            "includes": "ChainBatch.run: proposals, reset quirks, ancestor_x (scipy inv) and "
-                        "accept per chain on the host + the fused device step",
+            "includes": "ChainBatch.run: proposals, reset quirks, ancestor_x (scipy getrf/getri in 4 "
+                        "InvPool worker processes) and accept per chain on the host + the fused device step",
+            "ms_per_step_serial_inv": 1e3 * e2e["serial"][0] / n_it,
+            "pool_bits_equal_serial": bool(np.array_equal(e2e["pool"][1], e2e["serial"][1])),
             "reference_cpu_s_per_chain_step": 1.2}
         if args.config == "C3":
             # BASELINE config C5 (128 x 5000, parent cap 6): the capped

@@ -132,6 +132,19 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
 int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
                              const double* d_anc, double sig0, double sig1, int cap, double* d_w_new,
                              double* d_ll1, double* d_ll_dag, int32_t* d_info, void* stream);
+/* nemo_optimal_weights as a queued call: _begin checks the context and
+ * pointers and returns at once; a library thread runs the queued calls in
+ * order (transfers, launches, the NEMO_ERR_OPT check); _end waits for the
+ * oldest call not yet ended and returns its result code (nemo_last_error()
+ * then holds its message).  The caller keeps every buffer alive and untouched
+ * until the matching _end, and makes no other call on ctx in between except
+ * further _begin / _end.  Replaces, like nemo_optimal_weights,
+ * get_optimal_weights(init=True) (nem_order_mcmc.py:172-208) for a caller
+ * that runs two chain groups in a pipeline (nemo/chains.py). */
+int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
+                               const double* anc, double sig0, double sig1, int cap, double* w_new,
+                               double* ll1, double* ll_dag, int32_t* info);
+int nemo_optimal_weights_end(nemo_ctx* ctx);
 /* order weights of chain `chain` from the last eval#1 of nemo_optimal_weights:
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);

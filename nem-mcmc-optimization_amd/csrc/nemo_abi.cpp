@@ -10,13 +10,38 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 using nemo::Ctx;
 
+// one queued nemo_optimal_weights call (nemo_optimal_weights_begin)
+struct StepJob {
+  int nchains, cap;
+  const int32_t* pos;
+  const double *w01, *anc;
+  double sig0, sig1;
+  double *w_new, *ll1, *ll_dag;
+  int32_t* info;
+  bool ran = false;
+  int rc = 0;
+  std::string err;
+};
+
 struct nemo_ctx {
   Ctx c;
+  // the asynchronous fused step: a library thread runs the queued calls in
+  // submission order; the caller collects them in the same order
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<StepJob*> jobs;  // submitted and not yet collected, oldest first
+  size_t next_run = 0;        // jobs[next_run..] have not started
+  bool stop = false;
 };
 
 namespace {
@@ -121,6 +146,15 @@ int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out)
 
 void nemo_ctx_destroy(nemo_ctx* ctx) {
   if (!ctx) return;
+  if (ctx->worker.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      ctx->stop = true;
+    }
+    ctx->cv.notify_all();
+    ctx->worker.join();
+  }
+  for (StepJob* j : ctx->jobs) delete j;
   Ctx& c = ctx->c;
   // teardown is best effort: a failure here has no caller left to report to
   (void)hipSetDevice(c.device);
@@ -130,7 +164,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_step};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c.h_stage) (void)hipHostFree(c.h_stage);
@@ -193,6 +227,20 @@ int host_stage(Ctx& c, size_t bytes) {
   }
   HIPCHK(hipHostMalloc(&c.h_stage, bytes, hipHostMallocDefault));
   c.h_stage_bytes = bytes;
+  return NEMO_OK;
+}
+
+// grow the device block that mirrors the staging layout to at least `bytes`
+int dev_stage(Ctx& c, size_t bytes) {
+  if (bytes <= c.d_step_bytes) return NEMO_OK;
+  HIPCHK(hipStreamSynchronize(c.stream));
+  if (c.d_step) {
+    HIPCHK(hipFree(c.d_step));
+    c.d_step = nullptr;
+    c.d_step_bytes = 0;
+  }
+  HIPCHK(hipMalloc(&c.d_step, bytes));
+  c.d_step_bytes = bytes;
   return NEMO_OK;
 }
 
@@ -644,29 +692,28 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
   const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
   // every transfer goes through the pinned staging buffer: [pos | w01 | anc |
-  // w_new | info | ll1 | ll_dag], each part 256-B aligned
+  // w_new | info | ll1 | ll_dag], each part 256-B aligned, and a device block
+  // with the same layout: one H2D of [pos .. info] (info preset to -1 = not a
+  // permissible pair) and one D2H of [w_new .. ll_dag]
   auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t o_w01 = up(n * S * 4), o_anc = o_w01 + up(n * S * S * 8), o_wn = o_anc + up(n * S * S * 8),
                o_inf = o_wn + up(n * S * S * 8), o_ll1 = o_inf + up(n * S * S * 4), o_lld = o_ll1 + up(n * 8),
                total = o_lld + up(n * 8);
   if ((rc = host_stage(c, total))) return rc;
+  if ((rc = dev_stage(c, total))) return rc;
   char* hs = (char*)c.h_stage;
+  char* ds = (char*)c.d_step;
   memcpy(hs, pos, n * S * 4);
   memcpy(hs + o_w01, w01, n * S * S * 8);
   memcpy(hs + o_anc, anc, n * S * S * 8);
   memcpy(hs + o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
-  HIPCHK(hipMemcpyAsync(c.d_pos, hs, n * S * 4, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c.d_w01, hs + o_w01, n * S * S * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c.d_anc, hs + o_anc, n * S * S * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c.d_wnew, hs + o_wn, n * S * S * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemsetAsync(c.d_info, 0xff, n * S * S * 4, st));
-  rc = nemo_optimal_weights_dev(ctx, nchains, c.d_pos, c.d_w01, c.d_anc, sig0, sig1, cap, c.d_wnew,
-                                c.d_ll, c.d_ll2, c.d_info, st);
+  memset(hs + o_inf, 0xff, n * S * S * 4);
+  HIPCHK(hipMemcpyAsync(ds, hs, o_ll1, hipMemcpyHostToDevice, st));
+  rc = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + o_w01),
+                                (const double*)(ds + o_anc), sig0, sig1, cap, (double*)(ds + o_wn),
+                                (double*)(ds + o_ll1), (double*)(ds + o_lld), (int32_t*)(ds + o_inf), st);
   if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(hs + o_wn, c.d_wnew, n * S * S * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hs + o_ll1, c.d_ll, n * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hs + o_lld, c.d_ll2, n * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hs + o_inf, c.d_info, n * S * S * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hs + o_wn, ds + o_wn, total - o_wn, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   memcpy(w_new, hs + o_wn, n * S * S * 8);
   memcpy(ll1, hs + o_ll1, n * 8);
@@ -685,6 +732,59 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
     }
   }
   return NEMO_OK;
+}
+
+// asynchronous form: the library thread runs each call's transfers, launches
+// and checks; the caller's thread only queues and, later, collects
+static void step_worker(nemo_ctx* ctx) {
+  std::unique_lock<std::mutex> lk(ctx->mu);
+  for (;;) {
+    ctx->cv.wait(lk, [ctx] { return ctx->stop || ctx->next_run < ctx->jobs.size(); });
+    if (ctx->stop) return;
+    StepJob* j = ctx->jobs[ctx->next_run];
+    lk.unlock();
+    j->rc = nemo_optimal_weights(ctx, j->nchains, j->pos, j->w01, j->anc, j->sig0, j->sig1, j->cap,
+                                 j->w_new, j->ll1, j->ll_dag, j->info);
+    if (j->rc) j->err = g_err;
+    lk.lock();
+    j->ran = true;
+    ++ctx->next_run;
+    ctx->cv.notify_all();
+  }
+}
+
+int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
+                               const double* anc, double sig0, double sig1, int cap, double* w_new,
+                               double* ll1, double* ll_dag, int32_t* info) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
+  if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  StepJob* j = new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info};
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!ctx->worker.joinable()) ctx->worker = std::thread(step_worker, ctx);
+    ctx->jobs.push_back(j);
+  }
+  ctx->cv.notify_all();
+  return NEMO_OK;
+}
+
+int nemo_optimal_weights_end(nemo_ctx* ctx) {
+  if (!ctx) return fail(NEMO_ERR_ARG, "null context");
+  StepJob* j;
+  {
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    if (ctx->jobs.empty()) return fail(NEMO_ERR_STATE, "no nemo_optimal_weights_begin to end");
+    j = ctx->jobs.front();
+    ctx->cv.wait(lk, [j] { return j->ran; });
+    ctx->jobs.pop_front();
+    --ctx->next_run;
+  }
+  const int rc = j->rc;
+  if (rc) g_err = j->err;
+  delete j;
+  return rc;
 }
 
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {

@@ -114,6 +114,9 @@ struct Ctx {
   // pinned memory plus a DMA copy costs a fraction of that
   void* h_stage = nullptr;
   size_t h_stage_bytes = 0;
+  // device mirror of the staging layout of nemo_optimal_weights (one copy each way)
+  void* d_step = nullptr;
+  size_t d_step_bytes = 0;
 
   // timing of the score kernel
   bool timing = false;

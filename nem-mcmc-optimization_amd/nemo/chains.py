@@ -55,27 +55,45 @@ def inv_stack(a):
     return out
 
 
-def _prepare(chains):
+def _prepare_start(chains, pool=None):
+    """First half of ``_prepare``.  With an ``InvPool`` the per-chain work
+    (expit, inversion, clip) starts in its workers."""
+    pos = np.stack([c._pos for c in chains]).astype(np.int32)
+    if pool is not None:
+        pool.start_prepare([c.parent_weights for c in chains], [c._mask for c in chains])
+        return pos, None
+    w = np.stack([c.parent_weights for c in chains])
+    mask = np.stack([c._mask for c in chains])
+    sig = w.copy()
+    sig[mask] = expit(w[mask])
+    eye = np.identity(chains[0].num_s)
+    return pos, (w, sig, np.clip(inv_stack(eye - sig) - eye, 0, 1))
+
+
+def _prepare_end(chains, part, pool=None):
+    pos, rest = part
+    if rest is None:
+        w = np.stack([c.parent_weights for c in chains])
+        sig, anc = pool.finish_prepare()
+    else:
+        w, sig, anc = rest
+    for k, c in enumerate(chains):
+        c.ll = 0.0
+        c.ancestor_x = anc[k]
+    return pos, w, sig, anc
+
+
+def _prepare(chains, pool=None):
     """Host inputs of ``get_optimal_weights`` for a group of chains: positions,
     weights, expit(weights) and ancestor_x = clip(inv(I - W~) - I, 0, 1) with W~
     the weights under expit on the permissible entries only
     (nem_order_mcmc.py:98-103, :185).  W~ doubles as the device's w01: the
     kernels read it at permissible (child, parent) entries only, where it is
     expit(W); expit runs on those entries alone (scipy's ufunc is elementwise,
-    so the bits are those of expit over the whole matrix)."""
-    s = chains[0].num_s
-    pos = np.stack([c._pos for c in chains]).astype(np.int32)
-    w = np.stack([c.parent_weights for c in chains])
-    mask = np.stack([c._mask for c in chains])
-    sig = w.copy()
-    sig[mask] = expit(w[mask])
-    w01 = sig
-    eye = np.identity(s)
-    anc = np.clip(inv_stack(eye - sig) - eye, 0, 1)
-    for k, c in enumerate(chains):
-        c.ll = 0.0
-        c.ancestor_x = anc[k]
-    return pos, w, w01, anc
+    so the bits are those of expit over the whole matrix).  The inversions run
+    in ``pool``'s worker processes when one is given (same LAPACK calls, same
+    bits: nemo/invpool.py)."""
+    return _prepare_end(chains, _prepare_start(chains, pool), pool)
 
 
 def _device_step(engine: Engine, prep, cap, raise_on_fail):
@@ -99,13 +117,13 @@ def _finish(chains, engine: Engine, prep, res, use_nem, cap):
     return out
 
 
-def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True):
+def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True, pool=None):
     """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
     chain in ONE fused device call; each chain's state is updated exactly as
     its own call would (same kernels, batch-invariant bits).  A failed local
     optimisation raises the reference's Exception (nem_order_mcmc.py:168-169);
     with ``raise_on_fail=False`` the step keeps the optimiser's last point."""
-    prep = _prepare(chains)
+    prep = _prepare(chains, pool)
     return _finish(chains, engine, prep, _device_step(engine, prep, cap, raise_on_fail), use_nem, cap)
 
 
@@ -122,7 +140,7 @@ def opt_weights_batch(chains, engine: Engine, cap=0):
 
 
 def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0,
-                raise_on_fail=True):
+                raise_on_fail=True, pool=None):
     """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
     lock-step: each MCMC step is one fused device call per chain group.  Chain k
     draws from ``chains[k].rng`` in the reference's call order, and ends with
@@ -130,10 +148,12 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     best_order, score lists, parents_list of the best order).  Returns the
     per-chain best scores.  If a local optimisation fails and
     ``raise_on_fail`` is set, the reference's Exception propagates and the
-    chains' states are unspecified afterwards (see the pipeline below)."""
+    chains' states are unspecified afterwards (see the pipeline below).
+    ``pool`` (an ``InvPool``) runs the ancestor_x inversions in worker
+    processes; the results do not change."""
     n = len(chains)
     s = chains[0].num_s
-    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail)
+    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail, pool=pool)
     curr = list(opt_weights_batch(chains, engine, cap=cap))
     st = []
     for k, c in enumerate(chains):
@@ -171,10 +191,13 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                 q["best_order_list"].append(q["best_order"])
 
     # Two chain groups in a software pipeline: the device step of one group
-    # runs in a worker thread (ctypes releases the GIL) while the host does
-    # the other group's accept / propose / reset / ancestor_x.  Chains are
-    # independent and results are batch-invariant, so the bits are those of
-    # one batch; use_nem scores on the device in the host phase, so it runs
+    # runs on the library's step thread (nemo_optimal_weights_begin / _end)
+    # while the host does the other group's accept / propose / reset /
+    # ancestor_x; the next group's step is queued before the running one
+    # ends, so the device goes from one group to the other without waiting
+    # for the host.
+    # Chains are independent and results are batch-invariant, so the bits are
+    # those of one batch; use_nem scores on the device in the host phase, so it runs
     # unpipelined.  A failed local optimisation of one group surfaces when
     # that group is finished, after the other group has already proposed its
     # next order: with raise_on_fail the exception leaves the chains' states
@@ -185,26 +208,35 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         for _ in range(n_iterations):
             propose(groups[0])
             post(groups[0], optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap,
-                                                  raise_on_fail=raise_on_fail))
+                                                  raise_on_fail=raise_on_fail, pool=pool))
     else:
-        from concurrent.futures import ThreadPoolExecutor
         pending = None
 
-        def finish(p):
-            idx, cs, prep, fut = p
-            post(idx, _finish(cs, engine, prep, fut.result(), False, cap))
+        def collect(p):
+            idx, cs, prep, call = p
+            call.end()
+            post(idx, _finish(cs, engine, prep, call.result(raise_on_fail), False, cap))
 
-        with ThreadPoolExecutor(max_workers=1) as ex:
+        try:
             for _ in range(n_iterations):
                 for idx in groups:
                     propose(idx)
                     cs = [chains[k] for k in idx]
-                    prep = _prepare(cs)
-                    if pending is not None:
-                        finish(pending)
-                    pending = (idx, cs, prep, ex.submit(_device_step, engine, prep, cap, raise_on_fail))
-            if pending is not None:
-                finish(pending)
+                    prep = _prepare_end(cs, _prepare_start(cs, pool), pool)
+                    pos, w, w01, anc = prep
+                    call = engine.bind_optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
+                    # queued behind the other group's step: the device goes from
+                    # one group to the other while the host accepts the other
+                    call.begin()
+                    p, pending = pending, (idx, cs, prep, call)
+                    if p is not None:
+                        collect(p)
+            p, pending = pending, None
+            if p is not None:
+                collect(p)
+        finally:
+            if pending is not None:   # an exception left a queued step: wait for it
+                pending[3].end()
     for k, c in enumerate(chains):
         q = st[k]
         c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]
@@ -226,10 +258,12 @@ class ChainBatch:
     local optimisation terminates abnormally -- at C3 most chains hit one
     within a few dozen steps, in the reference as here; the chains' states
     are unspecified after that exception.  ``"continue"`` keeps the
-    optimiser's last point and goes on (an extension for long runs)."""
+    optimiser's last point and goes on (an extension for long runs).
+    ``inv_pool`` (an ``InvPool``, shareable among batches) runs the per-step
+    ancestor_x inversions in worker processes: same bits, less host time."""
 
     def __init__(self, nem, init_orders, seeds, engine: Engine | None = None, gamma=None,
-                 swap_prob=0.95, use_nem=False, cap=0, on_fail="raise"):
+                 swap_prob=0.95, use_nem=False, cap=0, on_fail="raise", inv_pool=None):
         if on_fail not in ("raise", "continue"):
             raise ValueError(f"on_fail={on_fail!r}: 'raise' or 'continue'")
         self.raise_on_fail = on_fail == "raise"
@@ -241,6 +275,9 @@ class ChainBatch:
         self.swap_prob = swap_prob
         self.use_nem = use_nem
         self.cap = cap
+        if inv_pool is not None and (inv_pool.s != nem.num_s or inv_pool.maxb < len(init_orders)):
+            raise ValueError("inv_pool: matrix size or capacity does not fit this batch")
+        self.inv_pool = inv_pool
         self.chains = []
         for order, seed in zip(init_orders, seeds):
             c = NEMOrderMCMC(nem, np.asarray(order), engine=self.engine, cap=cap)
@@ -254,7 +291,7 @@ class ChainBatch:
         (best scores [n], best orders [n, S])."""
         self.best_scores = run_methods(self.chains, self.gammas, n_iterations, self.engine,
                                        swap_prob=self.swap_prob, use_nem=self.use_nem, cap=self.cap,
-                                       raise_on_fail=self.raise_on_fail)
+                                       raise_on_fail=self.raise_on_fail, pool=self.inv_pool)
         self.best_orders = [np.asarray(c.best_order).copy() for c in self.chains]
         self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(n_iterations, self.n)
         return self.best_scores, np.stack(self.best_orders)

@@ -155,23 +155,17 @@ class Engine:
 
         Returns (w_new, ll1, ll_dag, info): w_new is ``w_prev`` with every
         permissible entry replaced by expit(x*)."""
-        pos = i32(np.atleast_2d(pos))
-        n = pos.shape[0]
-        w01 = f64(w01).reshape(n, self.S, self.S)
-        anc = f64(anc).reshape(n, self.S, self.S)
-        w_new = np.array(w_prev, dtype=np.float64, copy=True).reshape(n, self.S, self.S)
-        ll1, lld = np.empty(n), np.empty(n)
-        info = np.empty((n, self.S, self.S), dtype=np.int32)
-        rc = _lib.load().nemo_optimal_weights(self._ctx, n, ptr(pos, _lib._i32p), ptr(w01), ptr(anc),
-                                              float(sig0), float(sig1), int(cap), ptr(w_new), ptr(ll1),
-                                              ptr(lld), ptr(info, _lib._i32p))
-        if rc == _lib.NEMO_ERR_OPT and not raise_on_fail:
-            return w_new, ll1, lld, info
-        if rc == _lib.NEMO_ERR_OPT:
-            # the reference raises a plain Exception (nem_order_mcmc.py:168-169)
-            raise Exception(_lib.load().nemo_last_error().decode())
-        check(rc)
-        return w_new, ll1, lld, info
+        call = self.bind_optimal_weights(pos, w01, anc, w_prev, sig0, sig1, cap=cap)
+        call.run()
+        return call.result(raise_on_fail)
+
+    def bind_optimal_weights(self, pos, w01, anc, w_prev, sig0, sig1, cap: int = 0):
+        """``optimal_weights`` in parts: the arguments are converted here;
+        ``run()`` is the library call, or ``begin()`` queues it on the library's
+        own step thread and ``end()`` waits for it (no Python thread, so no GIL
+        hand-over); ``result(raise_on_fail)`` returns what ``optimal_weights``
+        returns."""
+        return _OptimalWeightsCall(self, pos, w01, anc, w_prev, sig0, sig1, cap)
 
     # -- fixed-order optimizers (methods.py) --------------------------------
     def _sweep(self, fn, pos, w, *extra, raise_on_fail=True):
@@ -281,3 +275,42 @@ def lse_full(cells: np.ndarray, device: int = 0):
         eng = _LseEngine(e, device)
         _LSE_ENGINES[(e, device)] = eng
     return eng.ll(cells, want=True)
+
+
+class _OptimalWeightsCall:
+    __slots__ = ("w_new", "ll1", "lld", "info", "_keep", "_fn", "_args", "rc")
+
+    def __init__(self, eng: Engine, pos, w01, anc, w_prev, sig0, sig1, cap):
+        pos = i32(np.atleast_2d(pos))
+        n, s = pos.shape[0], eng.S
+        w01 = f64(w01).reshape(n, s, s)
+        anc = f64(anc).reshape(n, s, s)
+        self.w_new = np.array(w_prev, dtype=np.float64, copy=True).reshape(n, s, s)
+        self.ll1, self.lld = np.empty(n), np.empty(n)
+        self.info = np.empty((n, s, s), dtype=np.int32)
+        self._keep = (pos, w01, anc)
+        self._fn = _lib.load().nemo_optimal_weights
+        self._args = (eng._ctx, n, ptr(pos, _lib._i32p), ptr(w01), ptr(anc), float(sig0), float(sig1),
+                      int(cap), ptr(self.w_new), ptr(self.ll1), ptr(self.lld), ptr(self.info, _lib._i32p))
+        self.rc = None
+
+    def run(self):
+        self.rc = self._fn(*self._args)
+
+    def begin(self):
+        """Queue the call on the library's step thread and return at once."""
+        check(_lib.load().nemo_optimal_weights_begin(*self._args))
+
+    def end(self):
+        """Wait for the oldest queued call (this one, when begun and ended in order)."""
+        self.rc = _lib.load().nemo_optimal_weights_end(self._args[0])
+
+    def result(self, raise_on_fail=True):
+        rc = self.rc
+        if rc == _lib.NEMO_ERR_OPT and not raise_on_fail:
+            return self.w_new, self.ll1, self.lld, self.info
+        if rc == _lib.NEMO_ERR_OPT:
+            # the reference raises a plain Exception (nem_order_mcmc.py:168-169)
+            raise Exception(_lib.load().nemo_last_error().decode())
+        check(rc)
+        return self.w_new, self.ll1, self.lld, self.info

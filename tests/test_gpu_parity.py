@@ -275,6 +275,16 @@ def test_chain_batch_equals_single_chains():
         assert np.array_equal(np.array(single.accepted), cb.accepted[:, k])
         assert b == best[k]
         assert np.array_equal(single.best_order, best_orders[k])
+    # ancestor_x inversions in worker processes: the same trajectories
+    from nemo.invpool import InvPool
+    pool = InvPool(16, 4, n_workers=2)
+    try:
+        cbp = ChainBatch(m, orders, seeds, swap_prob=0.95, engine=cb.engine, inv_pool=pool)
+        bp, bop = cbp.run(8)
+    finally:
+        pool.close()
+    assert np.array_equal(bp, best) and np.array_equal(bop, best_orders)
+    assert np.array_equal(cbp.accepted, cb.accepted)
 
 
 @pytest.mark.parametrize("name,s,e,cap", [("net2", 11, 184, 0), ("C2", 16, 500, 0), ("C3", 64, 2000, 0),
@@ -612,3 +622,32 @@ def test_init_false_reoptimises_only_pairs_touching_i1_i2():
     assert redo.any() and (mask & ~touch).any()
     assert np.array_equal(part.parent_weights[mask & ~touch], w0[mask & ~touch])
     assert np.array_equal(part.parent_weights[redo], full.parent_weights[redo])
+
+
+def test_queued_fused_step_equals_direct_call():
+    """nemo_optimal_weights_begin / _end (the library's step thread): two
+    queued calls give the direct call's outputs and result codes, in order;
+    an _end with nothing queued is NEMO_ERR_STATE."""
+    from nemo import _lib
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m = generator.synthetic_nem(64, 2000, 3)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(21)
+    calls, direct = [], []
+    for n in (3, 5):
+        pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
+        w = rng.uniform(-3, 3, (n, 64, 64))
+        anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
+        direct.append(eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False))
+        calls.append(eng.bind_optimal_weights(pos, expit(w), anc, w, SIG0, SIG1))
+    for c in calls:
+        c.begin()
+    for c, d in zip(calls, direct):
+        c.end()
+        assert c.rc in (0, _lib.NEMO_ERR_OPT)
+        for x, y in zip(c.result(raise_on_fail=False), d):
+            assert np.array_equal(x, y)
+    assert _lib.load().nemo_optimal_weights_end(eng._ctx) == _lib.NEMO_ERR_STATE
+    # a queued call still running when the engine closes is waited for
+    calls[0].begin()
+    eng.close()
