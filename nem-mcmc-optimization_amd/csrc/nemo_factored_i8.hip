@@ -222,6 +222,16 @@ __device__ __forceinline__ double wsum_dpp(double v) {
   return rowsum4(v);
 }
 
+// sum over each 16-lane row, in every lane of the row (wsum_dpp's first four
+// stages): 12 VALU against ~50 for a 64-lane ds_bpermute tree
+__device__ __forceinline__ double rowsum16(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return v;
+}
+
 // Delta digits of one pair in integers: x = Delta 2^(6-c) in (-32, 32),
 // h = rint(x 2^18), l = rint((x 2^18 - h) 2^24) (both |.| <= 2^23, the first
 // difference exact by fma), x = h 2^-18 + l 2^-42 + <= 2^-43; then four
@@ -1105,8 +1115,10 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
         lexp += __builtin_amdgcn_frexp_exp(lprod);
         lprod = __builtin_amdgcn_frexp_mant(lprod);
         if (setn != set) {  // set complete: one partial
-          double v = log(lprod) + (double)lexp * 0.69314718055994530942;
-          v = wsum(lane < 16 ? v : 0.0);
+          // every 16-lane row holds the 16 column products (rowsum4): log_fast
+          // (lprod is a mantissa in [0.5, 1)) and a DPP sum within the row
+          double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
+          v = rowsum16(v);
           if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
           lprod = 1.0;
           lexp = 0;
@@ -1222,8 +1234,10 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
         lexp += __builtin_amdgcn_frexp_exp(lprod);
         lprod = __builtin_amdgcn_frexp_mant(lprod);
         if (setn != set) {  // set complete: one partial
-          double v = log(lprod) + (double)lexp * 0.69314718055994530942;
-          v = wsum(lane < 16 ? v : 0.0);
+          // every 16-lane row holds the 16 column products (rowsum4): log_fast
+          // (lprod is a mantissa in [0.5, 1)) and a DPP sum within the row
+          double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
+          v = rowsum16(v);
           if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
           lprod = 1.0;
           lexp = 0;

@@ -2,9 +2,10 @@
 
     python -m nemo.build            # from nem-mcmc-optimization_amd/
 
-One hipcc invocation compiles the kernels and the C-ABI into a shared library
-next to this file, so the built object travels with the repository snapshot to
-the GPU box.  The build is skipped when the library is newer than every source.
+hipcc compiles each kernel / C-ABI source to an object (in parallel, one
+process per source) and links them into a shared library next to this file,
+so the built object travels with the repository snapshot to the GPU box.  The
+build is skipped when the library is newer than every source.
 """
 from __future__ import annotations
 
@@ -13,6 +14,8 @@ import os
 import shutil
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 SRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
@@ -50,16 +53,24 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     target = out or LIB
     if not force and out is None and up_to_date():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", SRC_DIR,
-           *[f"-D{d}" for d in defines], "-o", target + ".tmp"] + _sources()
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    proc = subprocess.run(cmd, capture_output=True, text=True)
-    if proc.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
-    if verbose and proc.stderr.strip():
-        print(proc.stderr, file=sys.stderr)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             "-I", INCLUDE, "-I", SRC_DIR, *[f"-D{d}" for d in defines]]
+    jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        proc = subprocess.run(cmd, capture_output=True, text=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"hipcc failed ({proc.returncode}):\n{proc.stdout}\n{proc.stderr}")
+        if verbose and proc.stderr.strip():
+            print(proc.stderr, file=sys.stderr)
+
+    with tempfile.TemporaryDirectory(prefix="nemo_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in _sources()]
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(run, [[hipcc(), *flags, "-c", src, "-o", o] for src, o in zip(_sources(), objs)]))
+        run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-o", target + ".tmp", *objs])
     os.replace(target + ".tmp", target)
     return target
 
