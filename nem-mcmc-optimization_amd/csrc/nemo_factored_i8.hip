@@ -35,6 +35,11 @@
 #ifndef NEMO_I8_ABLATE
 #define NEMO_I8_ABLATE 0
 #endif
+// score_i8l_kernel's two-tile walk: the remainder R through slice 4's C-init
+// (1) or formed after the MFMAs (0; the round-2 form, same bits)
+#ifndef NEMO_I8L_RINIT
+#define NEMO_I8L_RINIT 1
+#endif
 // register budget: waves per SIMD the int8 score kernel is compiled for
 #ifndef NEMO_I8_WAVES_PER_SIMD
 #define NEMO_I8_WAVES_PER_SIMD 2
@@ -741,6 +746,12 @@ __device__ __forceinline__ double exp2_fx_series(uint32_t t0, int t1) {
   const double r = (double)(int)rr;
   return fma(r, fma(r, kL2C2, kL2C1), kL2C0);
 }
+// the same series from R itself (score_i8l_kernel's two-tile walk forms R
+// through slice 4's C-init)
+__device__ __forceinline__ double exp2_fx_series_r(int rr) {
+  const double r = (double)rr;
+  return fma(r, fma(r, kL2C2, kL2C1), kL2C0);
+}
 __device__ __forceinline__ double exp2_fx_apply(uint32_t t0, uint64_t ev, double p, double acc) {
   // (one v_bitop3: bits 9-19 of T_0 cancel the index the entry carries)
   const uint32_t hi = (t0 & ~511u) ^ (uint32_t)(ev >> 32);
@@ -1188,6 +1199,55 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
             h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h1a, 0, 0, 0);
             h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h1b, 0, 0, 0);
           }
+#if NEMO_I8L_RINIT
+          // slices 5-6 first; then T_0 of both tiles and their table reads, and
+          // the remainder's upper part (T_0 & 511) 2^6 becomes the C-init of
+          // slice 4, so R = l0 2^12 + l1 is one shift-add (the same integer R
+          // as exp2_fx_series forms, so the same bits; one VOP3 less per cell)
+          {
+            const i32x4 a = A(5);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(6);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
+          }
+          uint32_t t0a[4], t0b[4];
+          uint64_t eva[4], evb[4];
+          i32x4 ma, mb;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            t0a[g] = ((uint32_t)h0a[g] << 12) + (uint32_t)h1a[g];
+            eva[g] = exp2_fx_load(t0a[g]);
+            ma[g] = (int)((t0a[g] & 511u) << 6);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            t0b[g] = ((uint32_t)h0b[g] << 12) + (uint32_t)h1b[g];
+            evb[g] = exp2_fx_load(t0b[g]);
+            mb[g] = (int)((t0b[g] & 511u) << 6);
+          }
+          {
+            const i32x4 a = A(4);
+            l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, ma, 0, 0, 0);
+            l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, mb, 0, 0, 0);
+          }
+          auto epi = [&](const uint32_t (&t0)[4], const uint64_t (&evv)[4], const i32x4 l0, const i32x4 l1,
+                         double& ls0, double& ls1) {
+            double pr[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) pr[g] = exp2_fx_series_r((int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+              else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+            }
+          };
+          epi(t0a, eva, l0a, l1a, la0, la1);
+          epi(t0b, evb, l0b, l1b, lb0, lb1);
+#else
           {
             const i32x4 a = A(4);
             l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, i32x4{0, 0, 0, 0}, 0, 0, 0);
@@ -1224,6 +1284,7 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
           };
           epi(h0a, h1a, l0a, l1a, la0, la1);
           epi(h0b, h1b, l0b, l1b, lb0, lb1);
+#endif
         }
         double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
         lprod *= t * 16 + col < E ? l : 1.0;
