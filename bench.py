@@ -48,7 +48,7 @@ def algorithmic_flops_per_eval(S, E, cap):
     return 2 * n_pairs(S, cap) * E
 
 
-def cpu_baseline(m, seconds=10.0):
+def cpu_baseline(m, seconds=10.0, config="C3"):
     """The oracle (numpy restatement of the reference's compute_cell_ratios +
     calculate_ll, nem_order_mcmc.py:79-93, same operation order) timed on
     this host, one thread."""
@@ -66,7 +66,7 @@ def cpu_baseline(m, seconds=10.0):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "evals/s", "cores": 1, "kind": "port",
-            "sample": f"{n} order-score evals of the 64x2000 C3 model in {dt:.1f} s: oracle numpy "
+            "sample": f"{n} order-score evals of the {m.num_s}x{m.num_e} {config} model in {dt:.1f} s: oracle numpy "
                       "loop form (reference operation order), one thread, this host"}
 
 
@@ -393,6 +393,14 @@ def main():
                             "(S*E exps/eval) beside the MFMAs: valu_bound (PMC, profiles/valu.json; "
                             "DESIGN.md 3.1e)",
                     "valu_bound": load_valu_bound(f"{args.config}:{tkey}:b{B}")}
+            if roof["traffic"]:
+                # the metric's HBM GB/s fraction: the kernel's PMC HBM bytes per
+                # launch (its only HBM stream is the w01 input) over this run's
+                # launch time -- far from 8 TB/s: the kernel is not memory-bound
+                hbm = roof["traffic"]["bytes_per_launch"] / (kern_ms / 1e3) / 1e9
+                roof["hbm_measured"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": hbm / HBM_PEAK_GBS,
+                                        "note": "PMC traffic per launch / HIP-event launch time"}
             if i8l:
                 # what the matrix cores actually execute: 7 v_mfma_i32_16x16x64_i8
                 # (2*16*16*64 ops each) per 16-child row block per 16-effect tile,
@@ -433,7 +441,7 @@ def main():
         }
         rec.update(extras)
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(m, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(m, args.cpu_seconds, args.config)
             if args.cpu_procs > 1:  # also all the host cores the round budget allows
                 rec["cpu_baseline_procs"] = cpu_baseline_procs(args.config, args.cpu_procs, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

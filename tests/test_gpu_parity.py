@@ -425,7 +425,8 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
     # auto is the log2 fixed-point offset kernel; its 8 and 4 waves per block,
-    # one or two effect tiles per iteration and 6 waves per SIMD give the same
+    # one or two effect tiles per iteration (16 forms the exp remainder after
+    # the MFMAs, the default through slice 4's C-init) and 6 waves per SIMD give the same
     # bits, and so do the natural-scale offset kernel's (7 / 8) and the
     # max-offset kernel's (4 / 6)
     assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
