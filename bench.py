@@ -342,6 +342,27 @@ def main():
             "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
             "includes": "H2D of pos/W/anc, eval#1 with order weights, 2016 L-BFGS-B local optima "
                         "per chain, eval#2 on binarised weights, D2H"}
+        # BASELINE C3 names ONE chain: what one chain sees per call -- a
+        # synchronous host-pointer order score (B = 1: the calculate_ll path of
+        # one sampler, H2D + kernel + D2H) and the fused step of one chain
+        lat = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            eng.score(pos[:1], w01[:1], cap=cap)
+            lat.append(time.perf_counter() - t0)
+        ts1 = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            eng.optimal_weights(pos_h[:1], expit(w_h[:1]), anc[:1], w_h[:1], SIG0, SIG1, cap=cap,
+                                raise_on_fail=False)
+            ts1.append(time.perf_counter() - t0)
+        extras["single_chain"] = {
+            "score_call_us": 1e6 * float(np.median(lat)), "evals_per_s_sequential": 1.0 / float(np.median(lat)),
+            "fused_step_ms": 1e3 * float(np.median(ts1)), "chain_steps_per_s": 1.0 / float(np.median(ts1)),
+            "reference_cpu_s_per_chain_step": 1.2,
+            "includes": "score_call_us: one synchronous nemo_score call for one (pos, W) from host "
+                        "arrays; fused_step_ms: nemo_optimal_weights for one chain (eval#1 with order "
+                        "weights, 2016 local optima, eval#2, transfers)"}
         # the whole sampler: 16 chains' host state machines (reference call order,
         # Python random) + one fused device call per step
         from nemo import utils as nutils
