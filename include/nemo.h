@@ -199,7 +199,9 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                one tile per iteration compiled for 6 waves per SIMD,
  *                16 = 8 waves with one tile per iteration (14 and 16 give
  *                10's bits);
- *                15 = the round-1 form of 9 (row bits re-read from LDS)
+ *                15 = the round-1 form of 9 (row bits re-read from LDS);
+ *                17 = 10's walk in persistent blocks that prep the next
+ *                evaluation's digits during the walk (10's bits)
  *   "factored"   (get only) 1 if the staged table is factorable
  *   "win"        (get only) 1 if the capped lookup-table kernel is staged
  *                (U - U[S] two-valued per row, partial sums in range)

@@ -537,7 +537,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const bool win = ll_only0 && c.win_ok && cap >= 1 && cap <= kWinMaxCap &&
                    (c.fact_kernel == 0 || c.fact_kernel == 9 || c.fact_kernel == 15);
   if ((c.fact_kernel == 9 || c.fact_kernel == 15) && !win) return hipErrorInvalidValue;
-  const bool i8_path = spad <= 64 && ((fk0 >= 4 && fk0 <= 8) || (fk0 >= 10 && fk0 <= 14) || fk0 == 16) && ll_only0 && c.d_B8;
+  const bool i8_path = spad <= 64 && ((fk0 >= 4 && fk0 <= 8) || (fk0 >= 10 && fk0 <= 14) || fk0 == 16 || fk0 == 17) && ll_only0 && c.d_B8;
   hipError_t err = hipSuccess;
   if (!i8_path && !win) {  // the int8 kernel derives its Delta digits itself
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
@@ -557,11 +557,12 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // 7 / 8 int8 with the offset log-sum-exp (4 / 8 waves), 10 / 11 the same in
   // log2 fixed point (8 / 4 waves; 12: 16 waves; 13: register-stationary;
   // 14: 8 waves compiled for 6 waves per SIMD; 10 walks two effect tiles per
-  // iteration, 16 is the same kernel with one); auto prefers 10, then 8
+  // iteration, 16 is the same kernel with one; 17: 10's walk in persistent
+  // blocks that prep the next evaluation during the walk); auto prefers 10, then 8
   const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   const bool ll_only = !d_cs && !d_cells && !d_ow;
   const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
-  const bool i8 = spad <= 64 && ((fk >= 4 && fk <= 8) || (fk >= 10 && fk <= 14) || fk == 16) && ll_only && c.d_B8;
+  const bool i8 = spad <= 64 && ((fk >= 4 && fk <= 8) || (fk >= 10 && fk <= 14) || fk == 16 || fk == 17) && ll_only && c.d_B8;
   int np = 0;
   bool finalized = false;
   const bool l2 = i8 && c.i8o_ok && c.i8l_ok && (fk >= 10 || c.fact_kernel == 0);
@@ -572,7 +573,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block, 10 / 11: log2
     // fixed point with 8 / 4 (auto: 8)
     // (10 and auto: 8 waves, two effect tiles per iteration; 16: one tile)
-    const int waves = fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : (fk == 12 ? 16 : (fk == 7 || fk == 11) ? 4 : (l2 ? -2 : 8));
+    const int waves = fk == 17 ? -3 : fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : (fk == 12 ? 16 : (fk == 7 || fk == 11) ? 4 : (l2 ? -2 : 8));
     err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, l2, st, &np, &finalized);
   } else if (i8 && fk <= 6) {
     // auto: 4 waves per block for large batches, 8 (fewer splits) below

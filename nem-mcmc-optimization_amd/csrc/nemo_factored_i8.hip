@@ -966,6 +966,189 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   return hipGetLastError();
 }
 
+// The two-tile walk of score_i8l_kernel over sets [set, s_end) step WAVES of
+// one evaluation (A fragments Al, G C-inits Gi, partials of evaluation b).
+// hook(it) runs between iterations it and it + 1 (it = 0, 1, ...) and returns
+// nothing the walk reads: score_i8p_kernel runs the next evaluation's digit
+// prep there.  Returns the number of iterations walked.
+template <int NR, int WAVES, class Hook>
+__device__ __forceinline__ int i8l_walk2(const i32x4* __restrict__ Al0, const i32x4* __restrict__ Gi,
+                                        const i32x4* __restrict__ Bt, const i32x4* __restrict__ Bt64,
+                                        int set, int s_end, int ntiles, int E, int col, int lane,
+                                        uint32_t a_lane, const double* __restrict__ nullsum,
+                                        double* __restrict__ partial, size_t b, int nsets,
+                                        const double2* __restrict__ ltab, Hook hook) {
+  constexpr int SPAD = NR * 16;
+  const int rg = lane >> 4;
+  int it = 0;
+  if (set < s_end) {
+    double lprod = 1.0;
+    int lexp = 0;
+    int t = 8 * set;
+    auto tend = [&](int st) { return min(ntiles, 8 * st + 8); };
+    int t2 = t + 1 < tend(set) ? t + 1 : t;
+    i32x4 bca = Bt[(size_t)t * kWave + lane], bca64 = Bt64[(size_t)t * kWave + lane];
+    i32x4 bcb = Bt[(size_t)t2 * kWave + lane], bcb64 = Bt64[(size_t)t2 * kWave + lane];
+    for (;;) {
+      uint32_t ao = a_lane;
+      asm volatile("" : "+v"(ao));
+      const i32x4* Al = Al0 + ao;
+      const bool two = t2 != t;
+      int tn = t + 2, setn = set;
+      if (tn >= tend(set)) {
+        setn = set + WAVES;
+        tn = 8 * setn;
+      }
+      const bool more = setn < s_end;
+      const int tla = more ? tn : t;
+      const int tlb = more ? (tn + 1 < tend(setn) ? tn + 1 : tn) : t;
+      const i32x4 b1a = bca, b64a = bca64, b1b = bcb, b64b = bcb64;
+      bca = Bt[(size_t)tla * kWave + lane];
+      bca64 = Bt64[(size_t)tla * kWave + lane];
+      bcb = Bt[(size_t)tlb * kWave + lane];
+      bcb64 = Bt64[(size_t)tlb * kWave + lane];
+      double la0 = 0.0, la1 = 0.0, lb0 = 0.0, lb1 = 0.0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+        const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+        auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
+        // slice by slice for both tiles: each A fragment dies after its two MFMAs
+        i32x4 h0a, h0b, h1a, h1b, l0a, l0b, l1a, l1b;
+        {
+          const i32x4 a = A(0);
+          h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(1);
+          h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h0a, 0, 0, 0);
+          h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h0b, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(2);
+          h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c0, 0, 0, 0);
+          h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c0, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(3);
+          h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h1a, 0, 0, 0);
+          h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h1b, 0, 0, 0);
+        }
+#if NEMO_I8L_RINIT
+        // slices 5-6 first; then T_0 of both tiles and their table reads, and
+        // the remainder's upper part (T_0 & 511) 2^6 becomes the C-init of
+        // slice 4, so R = l0 2^12 + l1 is one shift-add (the same integer R
+        // as exp2_fx_series forms, so the same bits; one VOP3 less per cell)
+        {
+          const i32x4 a = A(5);
+          l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
+          l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(6);
+          l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
+          l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
+        }
+        uint32_t t0a[4], t0b[4];
+        uint64_t eva[4], evb[4];
+        i32x4 ma, mb;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          t0a[g] = ((uint32_t)h0a[g] << 12) + (uint32_t)h1a[g];
+          eva[g] = exp2_fx_load(t0a[g]);
+          ma[g] = (int)((t0a[g] & 511u) << 6);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          t0b[g] = ((uint32_t)h0b[g] << 12) + (uint32_t)h1b[g];
+          evb[g] = exp2_fx_load(t0b[g]);
+          mb[g] = (int)((t0b[g] & 511u) << 6);
+        }
+        {
+          const i32x4 a = A(4);
+          l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, ma, 0, 0, 0);
+          l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, mb, 0, 0, 0);
+        }
+        auto epi = [&](const uint32_t (&t0)[4], const uint64_t (&evv)[4], const i32x4 l0, const i32x4 l1,
+                       double& ls0, double& ls1) {
+          double pr[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pr[g] = exp2_fx_series_r((int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+            else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+          }
+        };
+        epi(t0a, eva, l0a, l1a, la0, la1);
+        epi(t0b, evb, l0b, l1b, lb0, lb1);
+#else
+        {
+          const i32x4 a = A(4);
+          l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, i32x4{0, 0, 0, 0}, 0, 0, 0);
+          l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, i32x4{0, 0, 0, 0}, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(5);
+          l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
+          l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
+        }
+        {
+          const i32x4 a = A(6);
+          l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
+          l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
+        }
+        auto epi = [&](const i32x4 h0, const i32x4 h1, const i32x4 l0, const i32x4 l1, double& ls0,
+                       double& ls1) {
+          uint32_t t0[4];
+          uint64_t evv[4];
+          double pr[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+            evv[g] = exp2_fx_load(t0[g]);
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+            else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+          }
+        };
+        epi(h0a, h1a, l0a, l1a, la0, la1);
+        epi(h0b, h1b, l0b, l1b, lb0, lb1);
+#endif
+      }
+      double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
+      lprod *= t * 16 + col < E ? l : 1.0;
+      lexp += __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      l = rowsum4(lb0 + lb1) + 1.0;
+      lprod *= two && t2 * 16 + col < E ? l : 1.0;
+      lexp += __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      if (setn != set) {  // set complete: one partial
+        // every 16-lane row holds the 16 column products (rowsum4): log_fast
+        // (lprod is a mantissa in [0.5, 1)) and a DPP sum within the row
+        double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
+        v = rowsum16(v);
+        if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+        lprod = 1.0;
+        lexp = 0;
+      }
+      hook(it++);
+      if (!more) break;
+      t = tn;
+      t2 = tlb;
+      set = setn;
+    }
+  }
+  return it;
+}
+
 // ---------------------------------------------------------------------------
 // score_i8l_kernel: score_i8o_kernel's contraction and offset log-sum-exp
 // with every table quantity in units of 1 / ln 2 (digits of Delta / ln 2,
@@ -1145,170 +1328,8 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
     // arithmetic per cell and the same order of the column products as TT = 1,
     // so the same bits.  The second tile of a set's odd tail repeats the first
     // and is not multiplied in.
-    if (set < s_end) {
-      double lprod = 1.0;
-      int lexp = 0;
-      int t = 8 * set;
-      auto tend = [&](int st) { return min(ntiles, 8 * st + 8); };
-      int t2 = t + 1 < tend(set) ? t + 1 : t;
-      i32x4 bca = Bt[(size_t)t * kWave + lane], bca64 = Bt64[(size_t)t * kWave + lane];
-      i32x4 bcb = Bt[(size_t)t2 * kWave + lane], bcb64 = Bt64[(size_t)t2 * kWave + lane];
-      for (;;) {
-        uint32_t ao = a_lane;
-        asm volatile("" : "+v"(ao));
-        const i32x4* Al = ev.A + ao;
-        const bool two = t2 != t;
-        int tn = t + 2, setn = set;
-        if (tn >= tend(set)) {
-          setn = set + WAVES;
-          tn = 8 * setn;
-        }
-        const bool more = setn < s_end;
-        const int tla = more ? tn : t;
-        const int tlb = more ? (tn + 1 < tend(setn) ? tn + 1 : tn) : t;
-        const i32x4 b1a = bca, b64a = bca64, b1b = bcb, b64b = bcb64;
-        bca = Bt[(size_t)tla * kWave + lane];
-        bca64 = Bt64[(size_t)tla * kWave + lane];
-        bcb = Bt[(size_t)tlb * kWave + lane];
-        bcb64 = Bt64[(size_t)tlb * kWave + lane];
-        double la0 = 0.0, la1 = 0.0, lb0 = 0.0, lb1 = 0.0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          const i32x4 c0 = Gi[(16 * r) / 4 + rg];
-          const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
-          auto A = [&](int sl) { return Al[(sl * SPAD + 16 * r) * 4]; };
-          // slice by slice for both tiles: each A fragment dies after its two MFMAs
-          i32x4 h0a, h0b, h1a, h1b, l0a, l0b, l1a, l1b;
-          {
-            const i32x4 a = A(0);
-            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, i32x4{0, 0, 0, 0}, 0, 0, 0);
-            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, i32x4{0, 0, 0, 0}, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(1);
-            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h0a, 0, 0, 0);
-            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h0b, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(2);
-            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c0, 0, 0, 0);
-            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c0, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(3);
-            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, h1a, 0, 0, 0);
-            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, h1b, 0, 0, 0);
-          }
-#if NEMO_I8L_RINIT
-          // slices 5-6 first; then T_0 of both tiles and their table reads, and
-          // the remainder's upper part (T_0 & 511) 2^6 becomes the C-init of
-          // slice 4, so R = l0 2^12 + l1 is one shift-add (the same integer R
-          // as exp2_fx_series forms, so the same bits; one VOP3 less per cell)
-          {
-            const i32x4 a = A(5);
-            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
-            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(6);
-            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
-            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
-          }
-          uint32_t t0a[4], t0b[4];
-          uint64_t eva[4], evb[4];
-          i32x4 ma, mb;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            t0a[g] = ((uint32_t)h0a[g] << 12) + (uint32_t)h1a[g];
-            eva[g] = exp2_fx_load(t0a[g]);
-            ma[g] = (int)((t0a[g] & 511u) << 6);
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            t0b[g] = ((uint32_t)h0b[g] << 12) + (uint32_t)h1b[g];
-            evb[g] = exp2_fx_load(t0b[g]);
-            mb[g] = (int)((t0b[g] & 511u) << 6);
-          }
-          {
-            const i32x4 a = A(4);
-            l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, ma, 0, 0, 0);
-            l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, mb, 0, 0, 0);
-          }
-          auto epi = [&](const uint32_t (&t0)[4], const uint64_t (&evv)[4], const i32x4 l0, const i32x4 l1,
-                         double& ls0, double& ls1) {
-            double pr[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) pr[g] = exp2_fx_series_r((int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
-              else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
-            }
-          };
-          epi(t0a, eva, l0a, l1a, la0, la1);
-          epi(t0b, evb, l0b, l1b, lb0, lb1);
-#else
-          {
-            const i32x4 a = A(4);
-            l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, i32x4{0, 0, 0, 0}, 0, 0, 0);
-            l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, i32x4{0, 0, 0, 0}, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(5);
-            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a, c1, 0, 0, 0);
-            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b, c1, 0, 0, 0);
-          }
-          {
-            const i32x4 a = A(6);
-            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a, l1a, 0, 0, 0);
-            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b, l1b, 0, 0, 0);
-          }
-          auto epi = [&](const i32x4 h0, const i32x4 h1, const i32x4 l0, const i32x4 l1, double& ls0,
-                         double& ls1) {
-            uint32_t t0[4];
-            uint64_t evv[4];
-            double pr[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
-              evv[g] = exp2_fx_load(t0[g]);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-              pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
-              else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
-            }
-          };
-          epi(h0a, h1a, l0a, l1a, la0, la1);
-          epi(h0b, h1b, l0b, l1b, lb0, lb1);
-#endif
-        }
-        double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
-        lprod *= t * 16 + col < E ? l : 1.0;
-        lexp += __builtin_amdgcn_frexp_exp(lprod);
-        lprod = __builtin_amdgcn_frexp_mant(lprod);
-        l = rowsum4(lb0 + lb1) + 1.0;
-        lprod *= two && t2 * 16 + col < E ? l : 1.0;
-        lexp += __builtin_amdgcn_frexp_exp(lprod);
-        lprod = __builtin_amdgcn_frexp_mant(lprod);
-        if (setn != set) {  // set complete: one partial
-          // every 16-lane row holds the 16 column products (rowsum4): log_fast
-          // (lprod is a mantissa in [0.5, 1)) and a DPP sum within the row
-          double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
-          v = rowsum16(v);
-          if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
-          lprod = 1.0;
-          lexp = 0;
-        }
-        if (!more) break;
-        t = tn;
-        t2 = tlb;
-        set = setn;
-      }
-    }
+    i8l_walk2<NR, WAVES>(ev.A, Gi, Bt, Bt64, set, s_end, ntiles, E, col, lane, a_lane, nullsum, partial, b,
+                         nsets, ltab, [](int) {});
   }
   if (split == 1) {
     __syncthreads();
@@ -1492,6 +1513,152 @@ __global__ __launch_bounds__(8 * kWave, NEMO_I8O_WAVES_PER_SIMD) void score_i8s_
   }
 }
 
+// ---------------------------------------------------------------------------
+// score_i8p_kernel (fact_kernel 17; an experiment, not auto): score_i8l_kernel's
+// two-tile walk in a persistent block that pipelines its evaluations.  In
+// score_i8l_kernel a block preps one evaluation's digits (global weight loads,
+// two log_fast and the digit split per pair; 19% of the launch on its own)
+// before it walks its tiles.  Here each block owns evaluations b, b + grid, ...
+// with two digit buffers: while the waves walk evaluation n from one buffer,
+// each wave preps its passes of evaluation n + 1 into the other after its first
+// walk iteration, so the prep's loads and logs interleave with the tiles; no
+// per-evaluation table copy.  Two block barriers per evaluation.  The per-set
+// arithmetic, the digits, G and the partial sum are score_i8l_kernel's own
+// code, so the bits are too.  Measured 7-13% SLOWER than score_i8l_kernel at
+// C3 whatever the prep point: one evaluation per block lets
+// the dispatcher backfill retiring blocks, which overlaps the preps already.
+// ---------------------------------------------------------------------------
+template <int NR, int WAVES>
+__global__ __launch_bounds__(WAVES * kWave, NEMO_I8L2_OCC) void score_i8p_kernel(
+    int S, int E, int ntiles, int nsets, int batch, int cap, double padg,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const int8_t* __restrict__ udig, const double* __restrict__ u0,
+    const double* __restrict__ nullsum, const void* __restrict__ tabs,
+    double* __restrict__ partial, double* __restrict__ ll_out) {
+  constexpr int SPAD = NR * 16;
+  constexpr int NSL = 7;
+  // one evaluation buffer: G [SPAD] f64, gi [2][SPAD], perm [SPAD], A [NSL][SPAD][4] x 16 B
+  constexpr int kBufG = 0, kBufGi = SPAD * 8, kBufPerm = kBufGi + 2 * SPAD * 4, kBufA = kBufPerm + SPAD * 4;
+  constexpr int kBuf = kBufA + NSL * SPAD * 64;
+  static_assert(kBufA % 16 == 0 && kBuf % 16 == 0, "16-B alignment of the A fragments");
+  extern __shared__ __attribute__((aligned(16))) double lds8[];
+  uint2* etab_o = (uint2*)lds8;                          // [kExpTabN] at LDS address 0
+  double2* ltab = (double2*)(etab_o + kExpTabN);         // [128] log table
+  double* elo_s = (double*)(ltab + 128);                 // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  char* bufs = (char*)(ehi_s + SPAD);                    // [2][kBuf]
+  auto evb = [&](int k) {
+    EvalLds e;
+    char* p = bufs + k * kBuf;
+    e.G = (double*)(p + kBufG);
+    e.perm = (int*)(p + kBufPerm);
+    e.A = (i32x4*)(p + kBufA);
+    return e;
+  };
+  auto gib = [&](int k) { return (int*)(bufs + k * kBuf + kBufGi); };
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int col = lane & 15, rg = lane >> 4;
+  const int nb = gridDim.x;
+  const int b0 = blockIdx.x;
+  if (b0 >= batch) return;  // (the launch never makes more blocks than evaluations)
+
+  auto set_perm = [&](int k, int e) {
+    int* perm = evb(k).perm;
+    for (int j = tid; j < S; j += blockDim.x) {
+      int pj = pos[(size_t)e * S + j];
+      pj = pj < 0 ? 0 : (pj >= S ? S - 1 : pj);  // malformed input must not fault
+      perm[pj] = j;
+    }
+  };
+  auto zero_a = [&](int k) {
+    i32x4* A = evb(k).A;
+    for (int q = tid; q < NSL * SPAD * 4; q += blockDim.x) A[q] = i32x4{0, 0, 0, 0};
+  };
+  auto diag = [&](int k) {  // U' / ln 2 as the free diagonal "parent" i of child i
+    int8_t* A8 = (int8_t*)evb(k).A;
+    for (int q = tid; q < S * NSL; q += blockDim.x) {
+      const int i = q / NSL, sl = q - i * NSL;
+      A8[sl * SPAD * 64 + a_byte<4>(i, i)] = udig[i * 8 + sl];
+    }
+  };
+  auto prep = [&](int k, int e) {  // this wave's passes of evaluation e into buffer k
+    constexpr int KB = 4;
+    const int npass = i8_npass(S, cap);
+    const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
+    for (int k0 = 0; k0 < my; k0 += KB)
+      i8o_prep_passes<SPAD, WAVES, KB, 4, true>(evb(k), k0, w, lane, S, cap, 0, w01 + (size_t)e * S * S,
+                                                elo_s, ehi_s, ltab);
+  };
+  auto finalize_g = [&](int k) {  // score_i8l_kernel's G + u0 split (see there)
+    const EvalLds ev = evb(k);
+    int* gi = gib(k);
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      const double g = i < S ? ev.G[i] + u0[i] : ev.G[i];
+      const double g0 = rint(g * kL2Scale);
+      gi[i] = (int)g0 + (1023 << 20);
+      gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 262144.0);
+    }
+  };
+
+  {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    const int4* src = (const int4*)tabs;
+    int4* dst = (int4*)lds8;
+    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+  }
+  for (int k = 0; k < 2; ++k) {
+    for (int i = tid; i < SPAD; i += blockDim.x) evb(k).G[i] = i < S ? 0.0 : padg;
+    zero_a(k);
+  }
+  set_perm(0, b0);
+  if (b0 + nb < batch) set_perm(1, b0 + nb);
+  __syncthreads();
+  diag(0);
+  diag(1);
+  __syncthreads();
+  prep(0, b0);
+  __syncthreads();
+  finalize_g(0);
+  __syncthreads();
+
+  const i32x4* Bt = (const i32x4*)B8;
+  const i32x4* Bt64 = Bt + (size_t)ntiles * kWave;  // the staged D1 bytes x 64
+  const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
+  int k = 0;
+  for (int e = b0; e < batch; e += nb, k ^= 1) {
+    const int en = e + nb;
+    bool pending = en < batch;
+    i8l_walk2<NR, WAVES>(evb(k).A, (const i32x4*)gib(k), Bt, Bt64, w, nsets, ntiles, E, col, lane, a_lane,
+                         nullsum, partial, (size_t)e, nsets, ltab, [&](int it) {
+                           if (pending && it == 0) {
+                             prep(k ^ 1, en);
+                             pending = false;
+                           }
+                         });
+    if (pending) prep(k ^ 1, en);  // a wave with no set to walk (nsets < 8)
+    __syncthreads();  // evaluation e walked (its partials written), en prepped
+    if (w == 0) {
+      const double v = sum_partials(partial + (size_t)e * nsets, nsets, lane);
+      if (lane == 0) ll_out[e] = v;
+    }
+    if (en < batch) finalize_g(k ^ 1);
+    const bool again = en + nb < batch;  // buffer k is refilled with evaluation en + nb
+    if (again) {
+      zero_a(k);
+      set_perm(k, en + nb);
+    }
+    __syncthreads();
+    if (again) diag(k);  // other bytes than the prep's, which may already run (next walk)
+  }
+}
+
 template <int NR>
 hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
@@ -1508,6 +1675,41 @@ hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
       c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
+  return hipGetLastError();
+}
+
+template <int NR>
+hipError_t launch_i8p_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                        double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  constexpr int SPAD = NR * 16;
+  const int ntiles = (c.E + 15) / 16;
+  const int nsets = (ntiles + 7) / 8;
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 2 * SPAD * 8 + 2 * ((size_t)SPAD * 20 + (size_t)7 * SPAD * 64);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, v = 0;
+    hipError_t ge = hipGetDevice(&dev);
+    if (ge == hipSuccess) ge = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ge != hipSuccess) return ge;
+    ncu = v > 0 ? v : 256;
+  }
+  if (lds > 65536) {  // past the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU)
+    hipError_t ae = hipFuncSetAttribute((const void*)score_i8p_kernel<NR, 8>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ae != hipSuccess) return ae;
+  }
+  // two resident blocks per CU (LDS: 2 x 77.5 KB at S = 64; VGPRs: 4 waves per SIMD)
+  // three blocks per CU in the grid (two are resident: LDS 2 x 77.5 KB at S =
+  // 64), so the third set of blocks starts as the first ones retire and the
+  // CU's blocks drift out of phase (1 / 2 / 3 per CU: 0.202 / 0.172 / 0.167 ms
+  // at C3, B = 2048); every wave preps at the start of its walk (staggered
+  // points measured the same or slower)
+  const int grid = std::min(batch, 3 * ncu);
+  score_i8p_kernel<NR, 8><<<dim3(grid), 8 * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, batch, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll);
+  *nparts = nsets;
+  *finalized = true;
   return hipGetLastError();
 }
 
@@ -1542,6 +1744,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
     if (l2)                                                                                    \
       return waves == 0 ? launch_i8s_t<NRV>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 16 ? launch_i8l_t<NRV, 16>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == -3 ? launch_i8p_t<NRV>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
            : waves == -8 ? launch_i8l_t<NRV, 8, 6>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == -2 ? launch_i8l_t<NRV, 8, NEMO_I8L2_OCC, 2>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \

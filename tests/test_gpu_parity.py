@@ -430,7 +430,7 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     # bits, and so do the natural-scale offset kernel's (7 / 8) and the
     # max-offset kernel's (4 / 6)
     assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
-    for fk in (10, 11, 12, 14, 16):
+    for fk in (10, 11, 12, 14, 16, 17):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
