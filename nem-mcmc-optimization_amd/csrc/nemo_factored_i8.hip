@@ -1685,14 +1685,11 @@ hipError_t launch_i8p_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   const int ntiles = (c.E + 15) / 16;
   const int nsets = (ntiles + 7) / 8;
   const size_t lds = kExpTabN * 8 + 128 * 16 + 2 * SPAD * 8 + 2 * ((size_t)SPAD * 20 + (size_t)7 * SPAD * 64);
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0, v = 0;
-    hipError_t ge = hipGetDevice(&dev);
-    if (ge == hipSuccess) ge = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ge != hipSuccess) return ge;
-    ncu = v > 0 ? v : 256;
-  }
+  int dev = 0, ncu = 0;
+  hipError_t ge = hipGetDevice(&dev);
+  if (ge == hipSuccess) ge = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (ge != hipSuccess) return ge;
+  if (ncu <= 0) ncu = 256;
   if (lds > 65536) {  // past the default 64 KB of dynamic LDS (gfx950 has 160 KB per CU)
     hipError_t ae = hipFuncSetAttribute((const void*)score_i8p_kernel<NR, 8>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
