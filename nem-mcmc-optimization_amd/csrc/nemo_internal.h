@@ -209,6 +209,54 @@ __device__ __forceinline__ double log_fast(double x, const double2* __restrict__
   return fma(kd, kLn2Hi, tj.y) + fma(kd, kLn2Lo, p);
 }
 
+// Cross-lane sums of a double without the LDS (DPP moves and permlane swaps are
+// VALU; __shfl_xor goes through ds_bpermute).
+// DPP move of a double (both dwords), dpp_ctrl CTRL over all rows / banks
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)b, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// sum over the four 16-lane rows (lanes col, col+16, col+32, col+48), in
+// every lane: v_permlane16_swap then v_permlane32_swap (both outputs kept)
+__device__ __forceinline__ double rowsum4(double v) {
+  uint64_t b = __builtin_bit_cast(uint64_t, v);
+  auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  double a0 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  double a1 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  v = a0 + a1;
+  b = __builtin_bit_cast(uint64_t, v);
+  lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+  hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  a0 = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+  a1 = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  return a0 + a1;
+}
+
+// sum over the wave in every lane, all VALU: quad xor 1 and 2 (quad_perm),
+// the 8-lane and 16-lane mirrors, then the permlane swaps across rows
+__device__ __forceinline__ double wsum_dpp(double v) {
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
+  return rowsum4(v);
+}
+
+// sum over each 16-lane row, in every lane of the row (wsum_dpp's first four
+// stages): 12 VALU against ~50 for a 64-lane ds_bpermute tree
+__device__ __forceinline__ double rowsum16(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return v;
+}
+
 // the 128-entry table of log_fast (2 KB of LDS), filled by a block
 __device__ __forceinline__ void fill_log_table(double2* ltab, int tid, int nthreads) {
   for (int k = tid; k < 128; k += nthreads) {

@@ -361,8 +361,7 @@ __global__ __launch_bounds__(WAVES * kWave, NEMO_WIN2_OCC) void score_window2_ke
       Rc = R[0];
     }
     double v = 64 * word + lane < E ? log_fast(1.0 + (s0 + s1), ltab) : 0.0;  // 1 = e^0 of the null row
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    v = wsum_dpp(v);  // DPP + permlane swaps: no ds_bpermute on the LDS this kernel is bound by
     if (lane == 0) partial[(size_t)b * nwords + word] = nullw[word] + v;
   }
   if (split == 1) {
