@@ -433,8 +433,11 @@ struct LocalObjective {
         p1 += log_fast(c[q] * e1 + 1.0, ltab);
       }
     }
-    p0 = wave_sum(p0);
-    p1 = wave_sum(p1);
+    // wave sums by DPP + permlane swaps (VALU): the f-evaluation is on the
+    // serial critical path of the line search, and a ds_bpermute tree adds
+    // six LDS round trips to it
+    p0 = wsum_dpp(p0);
+    p1 = wsum_dpp(p1);
     // nem_order_mcmc.py:20-22: (-sum + |ex - anc|) + ex*(1 - ex)
     f0 = (-p0 + fabs(e0 - anc)) + e0 * (1.0 - e0);
     f1 = (-p1 + fabs(e1 - anc)) + e1 * (1.0 - e1);
