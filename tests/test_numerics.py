@@ -175,6 +175,63 @@ def test_exp2_fixed_point_assembly():
     assert worst <= 3.2e-13
 
 
+def test_remainder_through_slice4_cinit():
+    """score_i8l_kernel's two-tile walk (NEMO_I8L_RINIT): slice 4's MFMA starts
+    from C = (T_0 & 511) 2^6, so R = l0' 2^12 + l1 in 32-bit wrap-around
+    arithmetic is exactly exp2_fx_series' R = (T_0 & 511) 2^18 + (l0 2^12 + l1)
+    over the accumulator ranges (|slice-4 sum| <= 65 * 128 * 1, |l1| <= 2^23)."""
+    rng = np.random.default_rng(12)
+    n = 200000
+    t0 = rng.integers(0, 1 << 31, n, dtype=np.int64)
+    l0 = rng.integers(-65 * 128, 65 * 128 + 1, n, dtype=np.int64)
+    l1 = rng.integers(-(1 << 23), (1 << 23) + 1, n, dtype=np.int64)
+    wrap = lambda v: ((v + (1 << 31)) % (1 << 32)) - (1 << 31)  # int32 two's complement
+    r_old = wrap((t0 & 511) * (1 << 18) + wrap(l0 * 4096 + l1))
+    l0c = wrap(l0 + (t0 & 511) * 64)  # the MFMA accumulates onto the C operand
+    r_new = wrap(l0c * 4096 + l1)
+    assert np.array_equal(r_old, r_new)
+
+
+def _dpp(v, ctrl):
+    """update_dpp over 64 lanes for the dpp_ctrl values nemo_internal.h uses."""
+    lane = np.arange(64)
+    base, i = lane & ~15, lane & 15
+    if ctrl == 0xB1:  # quad_perm [1,0,3,2]
+        src = lane ^ 1
+    elif ctrl == 0x4E:  # quad_perm [2,3,0,1]
+        src = lane ^ 2
+    elif ctrl == 0x141:  # row_half_mirror
+        src = base + (i & 8) + (7 - (i & 7))
+    elif ctrl == 0x140:  # row_mirror
+        src = base + (15 - i)
+    else:
+        raise ValueError(ctrl)
+    return v[src]
+
+
+def _rowsum4(v):
+    """v_permlane16_swap then v_permlane32_swap, both outputs summed: every lane
+    gets the sum over lanes (l & 15) + 16 k."""
+    lane = np.arange(64)
+    v = v + v[lane ^ 16]
+    return v + v[lane ^ 32]
+
+
+def test_dpp_wave_sums_cover_every_lane_once():
+    """rowsum16 / wsum_dpp (nemo_internal.h): with integer-valued lanes (exact
+    sums), rowsum16 leaves each 16-lane row's sum in all its lanes and wsum_dpp
+    the wave's sum in every lane -- each lane counted exactly once."""
+    rng = np.random.default_rng(13)
+    for _ in range(50):
+        x = rng.integers(-1000, 1000, 64).astype(np.float64)
+        r = x.copy()
+        for c in (0xB1, 0x4E, 0x141, 0x140):
+            r = r + _dpp(r, c)
+        rows = x.reshape(4, 16).sum(axis=1)
+        assert np.array_equal(r, np.repeat(rows, 16))
+        assert np.array_equal(_rowsum4(r), np.full(64, x.sum()))
+
+
 # --- score_window2_kernel (nemo_window.hip): register walk of the capped tables ---
 
 _MLO = {16: 0x0000FFFF, 8: 0x00FF00FF, 4: 0x0F0F0F0F, 2: 0x33333333, 1: 0x55555555}
