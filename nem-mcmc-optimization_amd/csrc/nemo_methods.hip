@@ -26,11 +26,9 @@ namespace nemo {
 
 namespace {
 
-__device__ __forceinline__ double wsum_m(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
-}
+// wave sum on the line searches' serial path: DPP + permlane swaps (VALU),
+// not a ds_bpermute tree (nemo_internal.h)
+__device__ __forceinline__ double wsum_m(double v) { return wsum_dpp(v); }
 
 // log for the objectives: the table log where it is defined, else the
 // library log (0 -> -inf, negative -> NaN, as numpy gives)
