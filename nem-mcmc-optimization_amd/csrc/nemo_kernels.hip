@@ -416,8 +416,10 @@ struct LocalObjective {
       for (int q = 0; q < NPL; q += 8) {
 #pragma unroll
         for (int u = 0; u < 8 && q + u < NPL; ++u) {  // NPL may be 4
-          m0 *= c[q + u] * e0 + 1.0;
-          m1 *= c[q + u] * e1 + 1.0;
+          // one FMA per factor (the reference rounds c e and + 1 separately;
+          // the product form already departs from its sum of logs)
+          m0 *= fma(c[q + u], e0, 1.0);
+          m1 *= fma(c[q + u], e1, 1.0);
         }
         k0 += __builtin_amdgcn_frexp_exp(m0);
         m0 = __builtin_amdgcn_frexp_mant(m0);
