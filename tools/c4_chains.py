@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--chains", type=int, default=128)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--inv-workers", type=int, default=4)
+    ap.add_argument("--inv-workers", type=int, default=8)
     a = ap.parse_args()
 
     import torch
