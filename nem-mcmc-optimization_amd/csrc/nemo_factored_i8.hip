@@ -1076,19 +1076,22 @@ __device__ __forceinline__ int i8l_walk2(const i32x4* __restrict__ Al0, const i3
         epi(h0b, h1b, l0b, l1b, lb0, lb1);
 #endif
       }
-      double l = rowsum4(la0 + la1) + 1.0;  // + e^0 of the null row
-      lprod *= t * 16 + col < E ? l : 1.0;
-      lexp += __builtin_amdgcn_frexp_exp(lprod);
-      lprod = __builtin_amdgcn_frexp_mant(lprod);
-      l = rowsum4(lb0 + lb1) + 1.0;
-      lprod *= two && t2 * 16 + col < E ? l : 1.0;
+      // both tiles' column sums in one pass (rowsum_pair): rows 0 / 2 of the
+      // wave then hold tile a's, rows 1 / 3 tile b's, and each lane keeps the
+      // product of its own tile's columns
+      const double l = rowsum_pair(la0 + la1, lb0 + lb1) + 1.0;  // + e^0 of the null row
+      const bool tb = (lane & 16) != 0;
+      const bool ok = (((tb ? t2 : t) * 16 + col) < E) & (two | !tb);  // branch-free (bitwise)
+      lprod *= ok ? l : 1.0;
       lexp += __builtin_amdgcn_frexp_exp(lprod);
       lprod = __builtin_amdgcn_frexp_mant(lprod);
       if (setn != set) {  // set complete: one partial
-        // every 16-lane row holds the 16 column products (rowsum4): log_fast
-        // (lprod is a mantissa in [0.5, 1)) and a DPP sum within the row
+        // row 0 holds the 16 column products of the set's a tiles, row 1 those
+        // of its b tiles: log_fast (lprod is a mantissa in [0.5, 1)), a DPP sum
+        // within each row, then row 0's sum + row 1's
         double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
         v = rowsum16(v);
+        v += __shfl_down(v, 16, kWave);
         if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
         lprod = 1.0;
         lexp = 0;

@@ -237,6 +237,26 @@ __device__ __forceinline__ double rowsum4(double v) {
   return a0 + a1;
 }
 
+// the column sums of two 16 x 16 tiles at once (lane = column + 16 row
+// group; a and b: each lane's sum over its rows of tile a / tile b): after
+// it, rows 0 and 2 of the wave hold tile a's sum over the four row groups
+// and rows 1 and 3 tile b's.  v_permlane16_swap(a, b) exchanges a's odd rows
+// with b's even rows, so out[0] + out[1] = (a0 + a1, b0 + b1, a2 + a3, b2 + b3)
+// by row; one v_permlane32_swap adds rows 0 + 2 and 1 + 3.  Six VALU for two
+// tiles against ten per tile for rowsum4.
+__device__ __forceinline__ double rowsum_pair(double a, double b) {
+  const uint64_t x = __builtin_bit_cast(uint64_t, a), y = __builtin_bit_cast(uint64_t, b);
+  auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)y, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(x >> 32), (uint32_t)(y >> 32), false, false);
+  const double v = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]) +
+                   __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  const uint64_t z = __builtin_bit_cast(uint64_t, v);
+  lo = __builtin_amdgcn_permlane32_swap((uint32_t)z, (uint32_t)z, false, false);
+  hi = __builtin_amdgcn_permlane32_swap((uint32_t)(z >> 32), (uint32_t)(z >> 32), false, false);
+  return __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]) +
+         __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+}
+
 // sum over the wave in every lane, all VALU: quad xor 1 and 2 (quad_perm),
 // the 8-lane and 16-lane mirrors, then the permlane swaps across rows
 __device__ __forceinline__ double wsum_dpp(double v) {

@@ -424,16 +424,25 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
-    # auto is the log2 fixed-point offset kernel; its 8 and 4 waves per block,
-    # one or two effect tiles per iteration (16 forms the exp remainder after
-    # the MFMAs, the default through slice 4's C-init) and 6 waves per SIMD give the same
-    # bits, and so do the natural-scale offset kernel's (7 / 8) and the
-    # max-offset kernel's (4 / 6)
+    # auto is the log2 fixed-point offset kernel walking two effect tiles per
+    # iteration (10; 17 is the same walk in persistent blocks): the two tiles'
+    # column products are kept by different lanes, so its bits differ in the
+    # last places from the one-tile walks -- 4 / 8 waves per block, 16 waves,
+    # 6 waves per SIMD (11 / 16 / 12 / 14), which give one another's bits; the
+    # natural-scale offset kernel's (7 / 8) and the max-offset kernel's (4 / 6)
+    # likewise
     assert eng.get_option("i8o") == 2 and eng.get_option("i8l") == 1
-    for fk in (10, 11, 12, 14, 16, 17):
+    for fk in (10, 17):
         eng.set_option("fact_kernel", fk)
         assert np.array_equal(eng.score(pos, w01), big)
         assert np.array_equal(eng.score(pos[:7], w01[:7]), big[:7])
+    eng.set_option("fact_kernel", 16)
+    one = eng.score(pos, w01)
+    assert np.max(np.abs(one - big)) <= 1e-9
+    for fk in (11, 12, 14):
+        eng.set_option("fact_kernel", fk)
+        assert np.array_equal(eng.score(pos, w01), one)
+        assert np.array_equal(eng.score(pos[:7], w01[:7]), one[:7])
     # the register-stationary kernel: its own bits (per-set sums in another
     # order), independent of the batch too
     eng.set_option("fact_kernel", 13)
