@@ -197,8 +197,8 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                iteration); 12 = the same with 16 waves per block,
  *                13 = its register-stationary variant, 14 = 8 waves with
  *                one tile per iteration compiled for 6 waves per SIMD,
- *                16 = 8 waves with one tile per iteration (14 and 16 give
- *                10's bits);
+ *                16 = 8 waves with one tile per iteration (11, 12, 14 and
+ *                16 give one another's bits, within 1e-11 of 10's);
  *                15 = the round-1 form of 9 (row bits re-read from LDS);
  *                17 = 10's walk in persistent blocks that prep the next
  *                evaluation's digits during the walk (10's bits)
