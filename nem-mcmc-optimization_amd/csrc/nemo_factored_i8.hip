@@ -941,8 +941,18 @@ __device__ __forceinline__ int i8l_walk2(const i32x4* __restrict__ Al0, const i3
     int t = 8 * set;
     auto tend = [&](int st) { return min(ntiles, 8 * st + 8); };
     int t2 = t + 1 < tend(set) ? t + 1 : t;
-    i32x4 bca = Bt[(size_t)t * kWave + lane], bca64 = Bt64[(size_t)t * kWave + lane];
-    i32x4 bcb = Bt[(size_t)t2 * kWave + lane], bcb64 = Bt64[(size_t)t2 * kWave + lane];
+    // the B fragments through a buffer resource: the lane's byte offset stays
+    // in one VGPR and the tile offset is scalar, so a prefetch is one
+    // buffer_load with no per-load address arithmetic (Bt64 follows Bt)
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)Bt, (short)0, 2 * ntiles * kWave * 16, 0x00020000);
+    const uint32_t bln = (uint32_t)lane * 16u;
+    auto bload = [&](int tile, int x64) {
+      return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           brs, bln, (x64 * ntiles + tile) * kWave * 16, 0));
+    };
+    i32x4 bca = bload(t, 0), bca64 = bload(t, 1);
+    i32x4 bcb = bload(t2, 0), bcb64 = bload(t2, 1);
     for (;;) {
       uint32_t ao = a_lane;
       asm volatile("" : "+v"(ao));
@@ -954,13 +964,13 @@ __device__ __forceinline__ int i8l_walk2(const i32x4* __restrict__ Al0, const i3
         tn = 8 * setn;
       }
       const bool more = setn < s_end;
-      const int tla = more ? tn : t;
-      const int tlb = more ? (tn + 1 < tend(setn) ? tn + 1 : tn) : t;
+      const int tla = __builtin_amdgcn_readfirstlane(more ? tn : t);
+      const int tlb = __builtin_amdgcn_readfirstlane(more ? (tn + 1 < tend(setn) ? tn + 1 : tn) : t);
       const i32x4 b1a = bca, b64a = bca64, b1b = bcb, b64b = bcb64;
-      bca = Bt[(size_t)tla * kWave + lane];
-      bca64 = Bt64[(size_t)tla * kWave + lane];
-      bcb = Bt[(size_t)tlb * kWave + lane];
-      bcb64 = Bt64[(size_t)tlb * kWave + lane];
+      bca = bload(tla, 0);
+      bca64 = bload(tla, 1);
+      bcb = bload(tlb, 0);
+      bcb64 = bload(tlb, 1);
       double la0 = 0.0, la1 = 0.0, lb0 = 0.0, lb1 = 0.0;
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
