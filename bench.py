@@ -30,6 +30,12 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F64_MFMA_PEAK_TF = 78.6  # v_mfma_f64_16x16x4_f64: 2048 FLOP / 64 busy cycles / SIMD (PMC-checked)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (MI355X_MICROARCH.md: 2x the ~2.5 PF BF16 rate)
+# VALU issue: 256 CUs x 4 SIMDs, one VALU instruction in flight per SIMD per
+# cycle at the 2.4 GHz max clock (MI355X_MICROARCH.md chip table); PMC
+# SQ_ACTIVE_INST_VALU counts the busy cycles in quad-cycles
+N_SIMD = 1024
+CLOCK_MAX_GHZ = 2.4
+LDS_PEAK_TBS = 150.0   # ds_read_b64/b128, every CU streaming (MI355X_MICROARCH.md LDS)
 PATHS = {"auto": 0, "stream": 1, "factored": 2}
 
 
@@ -119,22 +125,20 @@ def cpu_baseline_procs(config, nproc=8, seconds=10.0):
                       "order), this host"}
 
 
-def load_valu_bound(key):
-    """PMC-derived VALU utilisation of the score kernel (profiles/valu.json,
-    tools/make_valu.py): VALU-busy cycles over SIMD cycles."""
-    p = os.path.join(HERE, "profiles", "valu.json")
+def load_record(name, key, build_id):
+    """A PMC record (profiles/valu.json: VALU / MFMA / LDS busy;
+    profiles/traffic.json: HBM bytes per launch) of the score kernel --
+    only if it was measured on THIS build of libnemo.so (its build id: a hash
+    of the sources and flags, nemo_build_id()); a record of another build is
+    stale and dropped."""
+    p = os.path.join(HERE, "profiles", name)
     if not os.path.exists(p):
         return None
     with open(p) as fh:
-        return json.load(fh).get(key)
-
-
-def load_traffic(key):
-    p = os.path.join(HERE, "profiles", "traffic.json")
-    if not os.path.exists(p):
+        rec = json.load(fh).get(key)
+    if not rec or rec.get("build_id") != build_id:
         return None
-    with open(p) as fh:
-        return json.load(fh).get(key)
+    return rec
 
 
 def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, world, dist,
@@ -243,6 +247,103 @@ def c5_capped(torch, dist, stream, batch=2048, steps=10, warmup_s=0.3):
     return out
 
 
+KERNEL_NAMES = {
+    "i8l": "score_i8l_kernel (x / ln 2 = Delta.D1 + U' + G exact in int8 fixed point on "
+           "v_mfma_i32_16x16x64_i8, 7 digit slices; e^x assembled from the integer accumulators + "
+           "table + degree-2 series; log-sum-exp offset by the null row; two 16-effect tiles per "
+           "iteration share the A fragments)",
+    "i8o": "score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
+           "fp64 cells, log-sum-exp offset by the null row)",
+    "i8": "score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, fp64 cells + "
+          "fused log-sum-exp)",
+    "factored": "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)",
+    "pipe": "score_factored_pipe_kernel (fp64 MFMA 16x16x4, U as the C-init, fused log-sum-exp)",
+    "win2": "score_window2_kernel (capped lookup tables walked from registers)",
+}
+ARITH = {
+    "i8l": "int8 fixed point 2^-38/ln2 + fp64 LSE",
+    "i8o": "int8 fixed point 2^-44 + fp64 LSE",
+    "i8": "int8 fixed point 2^-44 + fp64 LSE",
+}
+
+
+def kernel_tag(fk):
+    """profiles/*.json key tag of the kernel fact_kernel ``fk`` launches."""
+    if fk in (10, 11, 12, 14, 16, 17):
+        return "i8l"
+    if fk == 13:
+        return "i8s"
+    if fk in (7, 8):
+        return "i8o"
+    if fk in (4, 5, 6):
+        return "i8"
+    if fk in (9,):
+        return "win2"
+    if fk in (2, 3):
+        return "pipe"
+    return "factored"
+
+
+def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
+    """The dominant kernel's roofline: the unit that binds it, priced against
+    that unit's peak, with the other units beside it as fractions <= 1."""
+    tag = kernel_tag(fk)
+    kern_s = kern_ms / 1e3
+    valu = load_record("valu.json", f"{config}:{tag}:b{B}", bid)
+    traffic = load_record("traffic.json", f"{config}:{tag}:b{B}", bid)
+    fpe = algorithmic_flops_per_eval(S, E, cap)
+    f64eq = B * fpe / kern_s / 1e12
+    secondary = {}
+    if tag in ("i8l", "i8o", "i8s"):
+        # the MFMAs the kernel issues: 7 (log2) or 8 v_mfma_i32_16x16x64_i8
+        # (2*16*16*64 ops each) per 16-child row block per 16-effect tile
+        nslice = 7 if tag != "i8o" else 8
+        ops = ((E + 15) // 16) * (4 if S > 32 else 2 if S > 16 else 1) * nslice * 32768
+        a = B * ops / kern_s / 1e12
+        secondary["int8_mfma"] = {"achieved": a, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                                  "frac": a / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops}
+    if traffic:
+        hbm = traffic["bytes_per_launch"] / kern_s / 1e9
+        secondary["hbm"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm / HBM_PEAK_GBS,
+                            "note": "PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / this run's launch time"}
+    if valu and "SQ_LDS_IDX_ACTIVE" in valu:
+        lds = valu["SQ_LDS_IDX_ACTIVE"] / kern_s / 1e12
+        peak = 256 * CLOCK_MAX_GHZ / 1e3
+        secondary["lds"] = {"achieved": lds, "peak": peak, "unit": "T LDS-busy CU-cycles/s", "frac": lds / peak,
+                            "bank_conflict_share": valu.get("SQ_LDS_BANK_CONFLICT", 0.0) / valu["SQ_LDS_IDX_ACTIVE"]}
+    roof = {"kernel": KERNEL_NAMES.get(tag, tag), "fact_kernel": fk, "kernel_avg_ms": kern_ms,
+            "kernel_avg_ms_launch_events": launch_ev_ms,
+            "traffic": traffic["bytes_per_launch"] / B if traffic else None,
+            "traffic_unit": "HBM bytes per evaluation (PMC, this build)" if traffic else None}
+    if valu and "SQ_ACTIVE_INST_VALU" in valu:
+        busy = 4.0 * valu["SQ_ACTIVE_INST_VALU"]        # SIMD-cycles with a VALU instruction issuing
+        a = busy / kern_s / 1e12
+        peak = N_SIMD * CLOCK_MAX_GHZ / 1e3
+        roof.update({"bound": "valu", "achieved": a, "peak": peak, "unit": "T VALU-busy SIMD-cycles/s",
+                     "frac": a / peak, "valu_busy_cycles_per_launch": busy,
+                     "pmc": {k: valu[k] for k in ("valu_busy", "mfma_busy", "lds_busy", "mfma_coexec_frac",
+                                                  "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_MFMA") if k in valu}})
+        roof["note"] = ("bound = the SIMD's VALU issue (the exp epilogue: S*E cells per evaluation): achieved = "
+                        "PMC VALU-busy SIMD-cycles per launch of this build (4 x SQ_ACTIVE_INST_VALU) / this run's "
+                        "HIP-event launch time, against 1024 SIMDs x 2.4 GHz (the max clock, so frac <= the PMC "
+                        "valu_busy at the clock the chip held); the other units in secondary")
+    elif "int8_mfma" in secondary:
+        roof.update({"bound": "mfma", **{k: secondary["int8_mfma"][k] for k in ("achieved", "peak", "unit", "frac")},
+                     "note": "no PMC record of this build (profiles/valu.json): the int8 matrix-core fraction; "
+                             "the VALU issue binds in every profiled build (DESIGN.md 3.1e)"})
+    else:
+        roof.update({"bound": "mfma", "achieved": f64eq, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                     "frac": f64eq / F64_MFMA_PEAK_TF, "note": "fp64 MFMA contraction 2*P*E FLOP per evaluation"})
+    roof["secondary"] = secondary
+    if tag in ("i8l", "i8o", "i8s", "i8"):
+        roof["fp64_equivalent"] = {
+            "achieved": f64eq, "unit": "TFLOP/s", "flops_per_eval": fpe, "vs_f64_mfma_peak": f64eq / F64_MFMA_PEAK_TF,
+            "note": "the contraction Delta.D1 priced as fp64 work (2*P*E FLOP/eval) against the fp64 MFMA peak: "
+                    "how far the int8 fixed-point reformulation is past an fp64 matrix-core roofline; not a "
+                    "hardware fraction"}
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,10 +355,12 @@ def main():
     ap.add_argument("--path", default=os.environ.get("NEMO_BENCH_PATH", "auto"), choices=list(PATHS))
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the stream-kernel and MCMC lines")
+    ap.add_argument("--no-extras", action="store_true", help="skip the stream-kernel, MCMC and C4 lines")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=8,
                     help="processes of the multi-process CPU baseline (1: off)")
+    ap.add_argument("--c4-chains", type=int, default=128, help="C4: chains over all ranks (0: off)")
+    ap.add_argument("--c4-steps", type=int, default=10, help="C4: timed MCMC steps")
     args = ap.parse_args()
 
     import torch
@@ -280,14 +383,16 @@ def main():
 
     from scipy.special import expit
 
-    from nemo import generator
+    from nemo import _lib, generator
     from nemo.engine import Engine
 
+    bid = _lib.build_id()
     S, E, seed, cap, dtype = generator.CONFIGS[args.config]
     m = generator.config_nem(args.config)
     eng = Engine.for_nem(m, device=local, dtype=dtype)
     eng.set_option("score_path", PATHS[args.path])
     factored = eng.factored and args.path != "stream"
+    fk, err_bound = eng.score_kernel(cap) if factored else (-1, 0.0)
     B = args.batch
     eng.reserve(B)
     rng = np.random.default_rng(1000 + rank)
@@ -309,6 +414,22 @@ def main():
     ll = d_ll.cpu().numpy()
 
     extras = {}
+    if not args.no_extras and args.c4_chains > 0 and args.config == "C3":
+        # BASELINE C4 on every rank: the chains sharded over the ranks, one
+        # ChainBatch per rank, one all-gather of (best score, best order) --
+        # over RCCL with device tensors at N > 1 on GPUs
+        from nemo.chains import run_c4
+        dev = torch.device("cuda", local) if backend == "nccl" and world > 1 else None
+        r = run_c4(m, eng, n_chains=args.c4_chains, steps=args.c4_steps, device=dev)
+        extras["c4_chains"] = {
+            **{k: v for k, v in r.items() if k not in ("scores", "orders")},
+            "workload": f"C4: {args.c4_chains} chains of the C3 model sharded over {world} rank(s), "
+                        f"{args.c4_steps} MCMC steps (reference method() loop per chain, one fused device "
+                        "step per MCMC step per rank), one all-gather of (best score, best order)",
+            "collective": (f"all_gather over {'RCCL' if backend == 'nccl' else backend}"
+                           if world > 1 else None),
+            "reference_cpu_s_per_chain_step": 1.2}
+
     if rank == 0 and not args.no_extras:
         # the generic streaming kernel on the same model (HBM-priced roofline)
         eng.set_option("score_path", 1)
@@ -317,13 +438,14 @@ def main():
                                   warmup_s=min(args.warmup_seconds, 0.3))
         bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
         ach = Bs * bpe / (k_s / 1e3) / 1e9
+        tr = load_record("traffic.json", f"{args.config}:stream:b{Bs}", bid)
         extras["stream_kernel"] = {
             "evals_per_s": Bs * 10 / w_s, "batch": Bs, "kernel_avg_ms": k_s,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "bytes_per_eval": bpe,
-                         "traffic": load_traffic(f"{args.config}:stream:b{Bs}"),
+                         "traffic": tr["bytes_per_launch"] / Bs if tr else None,
                          "note": "the 65.5 MB exp(T) table is Infinity-Cache resident at C3, so "
-                                 "algorithmic bytes exceed HBM bytes (traffic = PMC bytes)"}}
+                                 "algorithmic bytes exceed HBM bytes (traffic = PMC HBM bytes per evaluation)"}}
         eng.set_option("score_path", PATHS[args.path])
         # fused per-step scorer of the sampler: 16 chains (C4 share of one GPU)
         from nemo.nem_order_mcmc import SIG0, SIG1
@@ -351,7 +473,7 @@ def main():
             eng.score(pos[:1], w01[:1], cap=cap)
             lat.append(time.perf_counter() - t0)
         ts1 = []
-        for _ in range(10):
+        for _ in range(20):
             t0 = time.perf_counter()
             eng.optimal_weights(pos_h[:1], expit(w_h[:1]), anc[:1], w_h[:1], SIG0, SIG1, cap=cap,
                                 raise_on_fail=False)
@@ -367,10 +489,11 @@ def main():
         # Python random) + one fused device call per step
         from nemo import utils as nutils
         from nemo.chains import ChainBatch
+        from nemo.invpool import InvPool, default_workers
         order0 = nutils.initial_order_guess(m.observed_knockdown_mat)
         seeds = [1234 + c for c in range(nch)]
-        from nemo.invpool import InvPool
-        pool = InvPool(S, nch, n_workers=4)
+        nw = default_workers(cap=4)
+        pool = InvPool(S, nch, n_workers=nw)
         n_it = 20
         e2e = {}
         for tag, pl in (("pool", pool), ("serial", None)):
@@ -384,7 +507,7 @@ def main():
         extras["mcmc_end_to_end"] = {
             "chains": nch, "steps": n_it, "ms_per_step": 1e3 * dt / n_it,
             "chain_steps_per_s": nch * n_it / dt,
-            "includes": "ChainBatch.run: proposals, reset quirks, ancestor_x (scipy getrf/getri in 4 "
+            "includes": f"ChainBatch.run: proposals, reset quirks, ancestor_x (scipy getrf/getri in {nw} "
                         "InvPool worker processes) and accept per chain on the host + the fused device step",
             "ms_per_step_serial_inv": 1e3 * e2e["serial"][0] / n_it,
             "pool_bits_equal_serial": bool(np.array_equal(e2e["pool"][1], e2e["serial"][1])),
@@ -396,66 +519,17 @@ def main():
 
     if rank == 0:
         if factored:
-            fpe = algorithmic_flops_per_eval(S, E, cap)
-            ach = B * fpe / (kern_ms / 1e3) / 1e12
-            fk = eng.get_option("fact_kernel")
-            i8l = S <= 64 and eng.get_option("i8l") > 0 and fk in (0, 10, 11, 12, 13, 14, 16)
-            i8o = not i8l and S <= 64 and eng.get_option("i8o") > 0 and fk in (0, 7, 8)
-            i8 = S <= 64 and (i8l or i8o or fk in (4, 5, 6))
-            kname = ("score_i8l_kernel (x / ln 2 = Delta.D1 + U' + G exact in int8 fixed point on "
-                     "v_mfma_i32_16x16x64_i8, 7 digit slices; e^x assembled from the integer "
-                     "accumulators + table + degree-2 series; log-sum-exp offset by the null row; "
-                     "two 16-effect tiles per iteration share the A fragments)"
-                     if i8l else
-                     "score_i8o_kernel (Delta.D1 + U - U[S] exact in int8 fixed point on "
-                     "v_mfma_i32_16x16x64_i8, fp64 cells, log-sum-exp offset by the null row)" if i8o else
-                     "score_i8_kernel (Delta.D1 exact in int8 fixed point on v_mfma_i32_16x16x64_i8, "
-                     "fp64 cells + fused log-sum-exp)" if i8 else
-                     "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)")
-            tkey = "i8l" if i8l else ("i8o" if i8o else ("i8" if i8 else "factored"))
-            roof = {"bound": "mfma", "achieved": ach, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                    "frac": ach / F64_MFMA_PEAK_TF,
-                    "traffic": load_traffic(f"{args.config}:{tkey}:b{B}"),
-                    "kernel": kname, "kernel_avg_ms": kern_ms, "flops_per_eval": fpe,
-                    "kernel_avg_ms_launch_events": launch_ev_ms,
-                    "note": "achieved = the algorithmic fp64 contraction Delta.D1 over the permissible "
-                            "pairs (2*P*E FLOP/eval) per kernel second (kernel_avg_ms: HIP events on the "
-                            "launch stream around the K timed launches / K; kernel_avg_ms_launch_events: "
-                            "the library's per-launch events on 20 more launches), priced against the dense fp64 "
-                            "MFMA peak (the arithmetic type of the path). The int8 kernels compute that "
-                            "contraction exactly in fixed point on the int8 matrix cores (score_i8l: 7 "
-                            "digit slices, 2^-38 / ln 2 per entry) and assemble e^x from the integer "
-                            "accumulators, so they can run faster than an fp64 MFMA contraction: frac "
-                            "> 1 means the reformulation beats the fp64 matrix roofline, not a "
-                            "measurement artefact. What binds is the SIMD issue of the VALU epilogue "
-                            "(S*E exps/eval) beside the MFMAs: valu_bound (PMC, profiles/valu.json; "
-                            "DESIGN.md 3.1e)",
-                    "valu_bound": load_valu_bound(f"{args.config}:{tkey}:b{B}")}
-            if roof["traffic"]:
-                # the metric's HBM GB/s fraction: the kernel's PMC HBM bytes per
-                # launch (its only HBM stream is the w01 input) over this run's
-                # launch time -- far from 8 TB/s: the kernel is not memory-bound
-                hbm = roof["traffic"]["bytes_per_launch"] / (kern_ms / 1e3) / 1e9
-                roof["hbm_measured"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": hbm / HBM_PEAK_GBS,
-                                        "note": "PMC traffic per launch / HIP-event launch time"}
-            if i8l:
-                # what the matrix cores actually execute: 7 v_mfma_i32_16x16x64_i8
-                # (2*16*16*64 ops each) per 16-child row block per 16-effect tile,
-                # against the dense int8 peak (2x BF16 per clock, ~5 POPS)
-                ops = ((E + 15) // 16) * (4 if S > 32 else 2 if S > 16 else 1) * 7 * 32768
-                roof["int8_mfma_executed"] = {
-                    "achieved": B * ops / (kern_ms / 1e3) / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
-                    "frac": B * ops / (kern_ms / 1e3) / 1e12 / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops,
-                    "note": "the matrix pipe is ~30% busy (PMC mfma_busy, valu_bound); the epilogue VALU issue binds"}
+            roof = score_roofline(args.config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid)
         else:
             bpe = algorithmic_bytes_per_eval(S, E, cap, 8 if dtype == "f64" else 4)
             ach = B * bpe / (kern_ms / 1e3) / 1e9
+            tr = load_record("traffic.json", f"{args.config}:stream:b{B}", bid)
             roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(f"{args.config}:stream:b{B}"),
+                    "frac": ach / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] / B if tr else None,
                     "kernel": "score_kernel (streams exp(T) rows)", "kernel_avg_ms": kern_ms,
-                    "kernel_avg_ms_launch_events": launch_ev_ms,
-                    "bytes_per_eval": bpe}
+                    "kernel_avg_ms_launch_events": launch_ev_ms, "bytes_per_eval": bpe}
+        roof["build_id"] = bid
+        tag = kernel_tag(fk) if factored else "stream"
         path = "factored" if factored else "stream"
         rec = {
             "metric": "order-score evals/sec (64 S-genes x 2000 effects); HBM GB/s fraction",
@@ -468,9 +542,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64" if dtype == "f64" else "f32",
+            "dtype": ARITH.get(tag, "f64" if dtype == "f64" else "f32"),
+            "ll_error_bound": err_bound,
+            "ll_error_bound_note": ("worst-case |ll error| of the kernel's fixed-point arithmetic for this "
+                                    "model (nemo_score_kernel; DESIGN.md 3.5a); auto keeps it within the "
+                                    "err_budget option (1e-7)"),
             "data": "synthetic (build-defined generator, SURVEY.md 8(d)); random orders, W~U(-3,3)",
-            "config": {"workload": f"{args.config}: S={S} E={E} cap={cap} {dtype}, {B} order-score "
+            "config": {"workload": f"{args.config}: S={S} E={E} cap={cap} {dtype} tables, {B} order-score "
                                    f"evaluations per step per GPU, {path} kernel",
                        "S": S, "E": E, "cap": cap, "batch_per_gpu": B, "path": path,
                        "parallelism": f"independent evaluations/chains sharded over {world} GPU(s); "

@@ -60,6 +60,9 @@ enum {
 
 const char* nemo_last_error(void);
 int nemo_version(void);
+/* identity of this build: a hash of the sources and compile flags it was
+ * built from (bench.py matches profiler records against it) */
+const char* nemo_build_id(void);
 /* number of visible HIP devices (0 on a host without GPU; never an error) */
 int nemo_device_count(int* count);
 
@@ -213,6 +216,28 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                (i8o = 2 and |Delta|, |U - U[S]| / ln 2 within its digit range) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
+
+/* ---- the fixed-point kernels' error budget ---------------------------------
+ * The int8 kernels round every entry of their contraction once (Delta of each
+ * permissible parent, the diagonal U entry, the row constant G); the roundings
+ * repeat over the effects, so their worst-case ll error grows with E:
+ *   |d ll| <= eps * sum_e (min(colbits_e, k) + 1) + E * series
+ * (colbits_e = staged rows whose D1 bit is set at effect e, k = S or cap + 1;
+ * eps = 2^-39 ln 2 for the log2 kernels 10-14, 16, 17, 2^(c - 49) for 4-8;
+ * DESIGN.md 3.5a).  Auto (fact_kernel 0) takes an int8 kernel only while that
+ * bound stays within "err_budget", else the next more precise one, down to
+ * the fp64 MFMA kernels.
+ *   f64 options: "err_budget" (get / set; default 1e-7, the north star's
+ *                1e-6 ll tolerance with a 10x margin);
+ *                "i8l_bound", "i8o_bound" (get only): the bound of the log2 /
+ *                natural-units kernels for an uncapped call on the staged model */
+int nemo_set_option_f64(nemo_ctx* ctx, const char* name, double value);
+int nemo_get_option_f64(nemo_ctx* ctx, const char* name, double* value);
+/* which fact_kernel a factored score call with this cap takes (ll_only: no
+ * cs / cells / order-weight outputs), with the worst-case |ll error| bound of
+ * its fixed-point arithmetic (0 for the fp64 kernels); *fact_kernel = -1 when
+ * the call takes the streaming kernel or the requested kernel cannot serve it */
+int nemo_score_kernel(nemo_ctx* ctx, int cap, int ll_only, int* fact_kernel, double* bound);
 
 /* ---- timing of the dominant (score) kernel, for bench.py ---------------- */
 int nemo_timing_enable(nemo_ctx* ctx, int enable);

@@ -10,11 +10,8 @@
 #include <string.h>
 
 #include <algorithm>
-#include <condition_variable>
-#include <deque>
-#include <mutex>
+#include <memory>
 #include <string>
-#include <thread>
 #include <vector>
 
 using nemo::Ctx;
@@ -27,7 +24,6 @@ struct StepJob {
   double sig0, sig1;
   double *w_new, *ll1, *ll_dag;
   int32_t* info;
-  bool ran = false;
   int rc = 0;
   std::string err;
 };
@@ -36,12 +32,8 @@ struct nemo_ctx {
   Ctx c;
   // the asynchronous fused step: a library thread runs the queued calls in
   // submission order; the caller collects them in the same order
-  std::thread worker;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<StepJob*> jobs;  // submitted and not yet collected, oldest first
-  size_t next_run = 0;        // jobs[next_run..] have not started
-  bool stop = false;
+  // (nemo_host.h StepQueue; created on the first _begin)
+  std::unique_ptr<nemo::host::StepQueue<StepJob>> steps;
 };
 
 namespace {
@@ -85,16 +77,8 @@ int check_ctx(nemo_ctx* ctx, bool need_staged) {
 
 // every row of pos must be a permutation of 0..S-1
 int check_pos(const int32_t* pos, int batch, int S) {
-  std::vector<char> seen(S);
-  for (int b = 0; b < batch; ++b) {
-    std::fill(seen.begin(), seen.end(), 0);
-    for (int i = 0; i < S; ++i) {
-      const int p = pos[(size_t)b * S + i];
-      if (p < 0 || p >= S || seen[p])
-        return fail(NEMO_ERR_ARG, "pos[%d] is not a permutation of 0..%d", b, S - 1);
-      seen[p] = 1;
-    }
-  }
+  const int b = nemo::host::first_bad_pos_row(pos, batch, S);
+  if (b >= 0) return fail(NEMO_ERR_ARG, "pos[%d] is not a permutation of 0..%d", b, S - 1);
   return NEMO_OK;
 }
 
@@ -146,15 +130,9 @@ int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out)
 
 void nemo_ctx_destroy(nemo_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->worker.joinable()) {
-    {
-      std::lock_guard<std::mutex> g(ctx->mu);
-      ctx->stop = true;
-    }
-    ctx->cv.notify_all();
-    ctx->worker.join();
-  }
-  for (StepJob* j : ctx->jobs) delete j;
+  // every queued step still runs (its caller's buffers are written), then the
+  // step thread ends; steps not collected with _end are dropped
+  if (ctx->steps) ctx->steps->shutdown();
   Ctx& c = ctx->c;
   // teardown is best effort: a failure here has no caller left to report to
   (void)hipSetDevice(c.device);
@@ -279,7 +257,9 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
   c.win_ok = false;
   c.fspad = nemo::factored_spad(c.S);
   c.nwords = nwords;
+  c.fx_colsum.clear();
   if (fact) {
+    c.fx_colsum = nemo::host::fixed_point_colsums(c.S, c.E, d1.data(), nwords);
     HIPCHK(dalloc(&c.d_D1w, d1.size()));
     HIPCHK(dalloc(&c.d_elo, S));
     HIPCHK(dalloc(&c.d_ehi, S));
@@ -378,28 +358,10 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
 
   // factored form: every off-diagonal row T[.][j] identical for all children
   // and two-valued (nem.py:44-46 builds exactly that); lo_j = its first value
-  const int nwords = (int)((E + 63) / 64);
-  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
-  std::vector<double> elo(S), ehi(S);
-  bool fact = true;
-  for (size_t j = 0; j < S && fact; ++j) {
-    const size_t i0 = (j == 0) ? 1 : 0;
-    const double* L = T + (i0 * S + j) * E;
-    for (size_t i = 0; i < S && fact; ++i)
-      if (i != j && i != i0 && memcmp(T + (i * S + j) * E, L, E * sizeof(double)) != 0) fact = false;
-    const double lo = L[0];
-    double hi = lo;
-    bool have_hi = false;
-    for (size_t e = 0; e < E && fact; ++e) {
-      const double v = L[e];
-      if (v == lo) continue;
-      if (!have_hi) { hi = v; have_hi = true; }
-      if (v != hi) { fact = false; break; }
-      d1[j * nwords + e / 64] |= 1ull << (e % 64);
-    }
-    elo[j] = exp(lo);
-    ehi[j] = exp(hi);
-  }
+  std::vector<uint64_t> d1;
+  std::vector<double> elo, ehi;
+  bool fact = nemo::host::detect_factored(c.S, c.E, T, d1, elo, ehi);
+  if (!fact) d1.assign((size_t)S * ((E + 63) / 64), 0ull);
   // the factored kernels' exp takes finite arguments: U must be finite too
   for (size_t k = 0; k < (S + 1) * E && fact; ++k)
     if (!isfinite(U[k]) || fabs(U[k]) > 1e9) fact = false;
@@ -430,13 +392,7 @@ int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
     return fail(NEMO_ERR_ARG, "|T| up to %g exceeds the %s product range (%g)", amax,
                 c.dtype == NEMO_F64 ? "f64" : "f32", lim);
   // the addition chains of compute_scores (nem.py:25-34), in its order
-  std::vector<double> chains(2 * (S + 1));
-  chains[0] = 0.0;
-  chains[S + 1] = B;
-  for (size_t k = 1; k <= S; ++k) {
-    chains[k] = chains[k - 1] + A;
-    chains[S + 1 + k] = chains[S + k] + A;
-  }
+  const std::vector<double> chains = nemo::host::knockdown_chains(c.S, A, B);
   // U's entries are chain elements: the ones indexed must be finite (NaN
   // cannot arise from finite A, B) and, for the factored kernels, <= 1e9
   bool ufin = true;
@@ -460,23 +416,9 @@ int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
 
   // factored form straight from D, with nemo_stage_tables' conventions:
   // lo_j = row j's first value, bit = "not lo_j"
-  const int nwords = (int)((E + 63) / 64);
-  std::vector<uint64_t> d1((size_t)S * nwords, 0ull);
-  std::vector<double> elo(S), ehi(S);
-  const double negA = -A;
-  for (size_t j = 0; j < S; ++j) {
-    const uint8_t* r = D + j * E;
-    const double lo = r[0] ? negA : B;
-    double hi = lo;
-    for (size_t e = 0; e < E; ++e) {
-      const double v = r[e] ? negA : B;
-      if (v == lo) continue;
-      hi = v;
-      d1[j * nwords + e / 64] |= 1ull << (e % 64);
-    }
-    elo[j] = exp(lo);
-    ehi[j] = exp(hi);
-  }
+  std::vector<uint64_t> d1;
+  std::vector<double> elo, ehi;
+  nemo::host::knockdown_factored(c.S, c.E, D, A, B, d1, elo, ehi);
   return stage_factored(ctx, ufin, d1, elo, ehi);
 }
 
@@ -736,23 +678,6 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
 
 // asynchronous form: the library thread runs each call's transfers, launches
 // and checks; the caller's thread only queues and, later, collects
-static void step_worker(nemo_ctx* ctx) {
-  std::unique_lock<std::mutex> lk(ctx->mu);
-  for (;;) {
-    ctx->cv.wait(lk, [ctx] { return ctx->stop || ctx->next_run < ctx->jobs.size(); });
-    if (ctx->stop) return;
-    StepJob* j = ctx->jobs[ctx->next_run];
-    lk.unlock();
-    j->rc = nemo_optimal_weights(ctx, j->nchains, j->pos, j->w01, j->anc, j->sig0, j->sig1, j->cap,
-                                 j->w_new, j->ll1, j->ll_dag, j->info);
-    if (j->rc) j->err = g_err;
-    lk.lock();
-    j->ran = true;
-    ++ctx->next_run;
-    ctx->cv.notify_all();
-  }
-}
-
 int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
                                const double* anc, double sig0, double sig1, int cap, double* w_new,
                                double* ll1, double* ll_dag, int32_t* info) {
@@ -760,31 +685,28 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
   if (rc) return rc;
   if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
   if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
-  StepJob* j = new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info};
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    if (!ctx->worker.joinable()) ctx->worker = std::thread(step_worker, ctx);
-    ctx->jobs.push_back(j);
+  std::string err;
+  try {
+    if (!ctx->steps)
+      ctx->steps.reset(new nemo::host::StepQueue<StepJob>([ctx](StepJob& j) {
+        j.rc = nemo_optimal_weights(ctx, j.nchains, j.pos, j.w01, j.anc, j.sig0, j.sig1, j.cap, j.w_new, j.ll1,
+                                    j.ll_dag, j.info);
+        if (j.rc) j.err = g_err;
+      }));
+    std::unique_ptr<StepJob> j(new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info});
+    if (ctx->steps->submit(std::move(j), &err)) return NEMO_OK;
+  } catch (const std::exception& e) {
+    err = e.what();
   }
-  ctx->cv.notify_all();
-  return NEMO_OK;
+  return fail(NEMO_ERR_STATE, "nemo_optimal_weights_begin: %s", err.c_str());
 }
 
 int nemo_optimal_weights_end(nemo_ctx* ctx) {
   if (!ctx) return fail(NEMO_ERR_ARG, "null context");
-  StepJob* j;
-  {
-    std::unique_lock<std::mutex> lk(ctx->mu);
-    if (ctx->jobs.empty()) return fail(NEMO_ERR_STATE, "no nemo_optimal_weights_begin to end");
-    j = ctx->jobs.front();
-    ctx->cv.wait(lk, [j] { return j->ran; });
-    ctx->jobs.pop_front();
-    --ctx->next_run;
-  }
-  const int rc = j->rc;
-  if (rc) g_err = j->err;
-  delete j;
-  return rc;
+  std::unique_ptr<StepJob> j = ctx->steps ? ctx->steps->collect() : nullptr;
+  if (!j) return fail(NEMO_ERR_STATE, "no nemo_optimal_weights_begin to end");
+  if (j->rc) g_err = j->err;
+  return j->rc;
 }
 
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
@@ -805,78 +727,6 @@ int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
 }  // extern "C"
 
 namespace {
-
-// order_arr (utils.py:173-188) arranges a matrix by argsort(order) = pos:
-// row/column a of M is node pos[a], so node i sits at index perm[i].
-// InverseMethod.opt_b's loop (methods.py:125-127) visits, for i = 0..S-1,
-// k = order[0 .. pos[i]-1].  Pair (i, k) moves M[a][b], a = perm[i],
-// b = perm[k]; only a > b is inside the lower triangle solve_triangular
-// reads.  Its objective reads B[a][b], i.e. the entries M[r][c] with
-// b ~> c and r ~> a in the graph of lower-triangle pairs (~> : reachable,
-// reflexive).  Levels: a pair goes after every earlier pair it reads and no
-// earlier than any earlier pair that reads it (those must see its old
-// value; a level reads before it commits).  One level = one launch.
-void build_inverse_schedule(Ctx& c, int nprob, const int32_t* pos) {
-  const int S = c.S;
-  const size_t n = (size_t)nprob * S;
-  if (c.inv_pos.size() == n && memcmp(c.inv_pos.data(), pos, n * 4) == 0) return;
-  c.inv_pos.assign(pos, pos + n);
-  std::vector<std::vector<int32_t>> levels;
-  c.inv_skip.clear();
-  const int W = (S + 63) / 64;
-  for (int b = 0; b < nprob; ++b) {
-    const int32_t* pb = pos + (size_t)b * S;
-    std::vector<int> perm(S);
-    for (int i = 0; i < S; ++i) perm[pb[i]] = i;
-    // pairs in loop order
-    std::vector<int> pa, pbb, pi, pk;
-    for (int i = 0; i < S; ++i)
-      for (int p = 0; p < pb[i]; ++p) {
-        const int k = perm[p];
-        const int ra = perm[i], rb = perm[k];
-        const int32_t ent = (b << 16) | (i << 8) | k;
-        if (ra > rb) {
-          pa.push_back(ra);
-          pbb.push_back(rb);
-          pi.push_back(ent);
-        } else {
-          c.inv_skip.push_back(ent);
-        }
-      }
-    // reach[x] bitset of y with y ~> x
-    std::vector<uint64_t> reach((size_t)S * W, 0ull);
-    std::vector<char> edge((size_t)S * S, 0);
-    for (size_t q = 0; q < pa.size(); ++q) edge[(size_t)pa[q] * S + pbb[q]] = 1;
-    for (int x = 0; x < S; ++x) {
-      uint64_t* rx = &reach[(size_t)x * W];
-      rx[x >> 6] |= 1ull << (x & 63);
-      for (int d = 0; d < x; ++d)
-        if (edge[(size_t)x * S + d])
-          for (int w = 0; w < W; ++w) rx[w] |= reach[(size_t)d * W + w];
-    }
-    auto r = [&](int x, int y) { return (reach[(size_t)x * W + (y >> 6)] >> (y & 63)) & 1ull; };
-    const size_t P = pa.size();
-    std::vector<int> lev(P, 0);
-    for (size_t p = 0; p < P; ++p) {
-      const int a2 = pa[p], b2 = pbb[p];
-      int l = 0;
-      for (size_t q = 0; q < p; ++q) {
-        const int a1 = pa[q], b1 = pbb[q];
-        if (r(b1, b2) && r(a2, a1)) l = std::max(l, lev[q] + 1);  // p reads q
-        if (r(b2, b1) && r(a1, a2)) l = std::max(l, lev[q]);      // q reads p
-      }
-      lev[p] = l;
-      if ((int)levels.size() <= l) levels.resize(l + 1);
-      levels[l].push_back(pi[p]);
-    }
-  }
-  c.inv_list.clear();
-  c.inv_level_off.assign(1, 0);
-  for (auto& lv : levels) {
-    c.inv_list.insert(c.inv_list.end(), lv.begin(), lv.end());
-    c.inv_level_off.push_back((int)c.inv_list.size());
-  }
-}
 
 int opt_status(const Ctx& c, const std::vector<int32_t>& inf, int nprob) {
   const size_t S = c.S;
@@ -971,20 +821,22 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
   Ctx& c = ctx->c;
   const size_t S = c.S;
   hipStream_t st = c.stream;
-  build_inverse_schedule(c, nprob, pos);
-  if (c.inv_list.size() > c.inv_list_cap) {
+  // levels of independent pairs that keep the reference's loop semantics
+  // (nemo_host.h build_inverse_schedule)
+  nemo::host::build_inverse_schedule(c.inv, c.S, nprob, pos);
+  if (c.inv.list.size() > c.inv_list_cap) {
     HIPCHK(hipStreamSynchronize(st));
-    HIPCHK(dalloc(&c.d_inv_list, c.inv_list.size()));
-    c.inv_list_cap = c.inv_list.size();
+    HIPCHK(dalloc(&c.d_inv_list, c.inv.list.size()));
+    c.inv_list_cap = c.inv.list.size();
   }
-  if (!c.inv_list.empty())
-    HIPCHK(hipMemcpyAsync(c.d_inv_list, c.inv_list.data(), c.inv_list.size() * 4, hipMemcpyHostToDevice, st));
+  if (!c.inv.list.empty())
+    HIPCHK(hipMemcpyAsync(c.d_inv_list, c.inv.list.data(), c.inv.list.size() * 4, hipMemcpyHostToDevice, st));
   // evaluation weights B/(1+B) (methods.py:118-121), evaluation (:122-123)
   HIPCHK(nemo::launch_ancestral(c, nprob, c.d_pos, c.d_wnew, c.d_w01, st));
   if ((rc = eval_with_ow(c, nprob, 0, c.d_w01, st))) return rc;
   // the pair loop (:125-127), level by level, optima committed into d_wnew
-  for (size_t l = 0; l + 1 < c.inv_level_off.size(); ++l) {
-    const int o0 = c.inv_level_off[l], o1 = c.inv_level_off[l + 1];
+  for (size_t l = 0; l + 1 < c.inv.level_off.size(); ++l) {
+    const int o0 = c.inv.level_off[l], o1 = c.inv.level_off[l + 1];
     HIPCHK(nemo::launch_inverse_level(c, o1 - o0, c.d_inv_list + o0, c.d_pos, c.d_wnew, c.d_ow, c.d_wdag,
                                       c.d_info, st));
   }
@@ -995,7 +847,7 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
   HIPCHK(hipStreamSynchronize(st));
   // pairs outside the lower triangle: B[a][b] = 0 whatever x, so the
   // objective is flat and L-BFGS-B stops at the clipped start (nit 0, 2 f-evals)
-  for (int32_t ent : c.inv_skip) {
+  for (int32_t ent : c.inv.skip) {
     const size_t idx = ((size_t)(ent >> 16) * S + ((ent >> 8) & 0xff)) * S + (ent & 0xff);
     w_out[idx] = std::min(std::max(w[idx], -5000.0), 500.0);
     inf[idx] = NEMO_LBFGSB_CONV_PGTOL | (2 << 16);
@@ -1049,6 +901,56 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
   return NEMO_OK;
+}
+
+int nemo_set_option_f64(nemo_ctx* ctx, const char* name, double value) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!name) return fail(NEMO_ERR_ARG, "null option name");
+  if (strcmp(name, "err_budget") == 0) {
+    if (!(value >= 0.0)) return fail(NEMO_ERR_ARG, "err_budget=%g must be >= 0", value);
+    ctx->c.err_budget = value;
+    return NEMO_OK;
+  }
+  return fail(NEMO_ERR_ARG, "unknown f64 option '%s'", name);
+}
+
+int nemo_get_option_f64(nemo_ctx* ctx, const char* name, double* value) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!name || !value) return fail(NEMO_ERR_ARG, "null argument");
+  const Ctx& c = ctx->c;
+  if (strcmp(name, "err_budget") == 0) {
+    *value = c.err_budget;
+    return NEMO_OK;
+  }
+  const bool l2 = strcmp(name, "i8l_bound") == 0, nat = strcmp(name, "i8o_bound") == 0;
+  if (l2 || nat) {
+    if (!c.staged || c.fx_colsum.empty()) return fail(NEMO_ERR_STATE, "no factored model staged");
+    *value = nemo::host::fixed_point_bound(l2 ? nemo::host::kFxLog2 : nemo::host::kFxNatural, c.i8_cexp,
+                                           c.fx_colsum, c.S, c.E, 0);
+    return NEMO_OK;
+  }
+  return fail(NEMO_ERR_ARG, "unknown f64 option '%s'", name);
+}
+
+int nemo_score_kernel(nemo_ctx* ctx, int cap, int ll_only, int* fact_kernel, double* bound) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (cap < 0 || !fact_kernel) return fail(NEMO_ERR_ARG, "cap=%d / null fact_kernel", cap);
+  const Ctx& c = ctx->c;
+  double b = 0.0;
+  *fact_kernel = use_factored(c) ? nemo::resolve_fact_kernel(c, cap, ll_only != 0, &b) : -1;
+  if (bound) *bound = b;
+  return NEMO_OK;
+}
+
+const char* nemo_build_id(void) {
+#ifdef NEMO_BUILD_ID
+  return NEMO_BUILD_ID;
+#else
+  return "unversioned";
+#endif
 }
 
 // ---------------------------------------------------------------------------

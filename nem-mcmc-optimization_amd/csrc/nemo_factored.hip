@@ -97,9 +97,6 @@ constexpr double kPadG = -1.0e6;
 // partial assignment (hence every bit of ll) does not depend on the batch
 constexpr int kPipeTilesPerWave = 8;
 
-// fact_kernel = 0 (auto) resolves to this for ll-only calls with S <= 64
-constexpr int kAutoFactKernel = 4;
-
 __device__ __forceinline__ int fxcd_work_index(int L, int N, int remap) {
   if (!remap) return L;
   const int x = L & 7, k = L >> 3;
@@ -524,22 +521,67 @@ int factored_partials(const Ctx& c) {
   return std::max(n, (c.E + 63) / 64);  // the lookup-table kernel: one per word
 }
 
+int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
+  if (bound) *bound = 0.0;
+  if (!c.factored) return -1;
+  if (cap >= c.S - 1) cap = 0;  // every predecessor is within the cap: no cap (same bits)
+  // the int8 kernels: S <= 64, ll only (they write no cs / cells / order weights)
+  const bool i8cap = c.fspad <= 64 && c.d_B8 && ll_only;
+  const bool wincap = ll_only && c.win_ok && cap >= 1 && cap <= kWinMaxCap;
+  auto bnd = [&](int kind) { return host::fixed_point_bound(kind, c.i8_cexp, c.fx_colsum, c.S, c.E, cap); };
+  int fk = c.fact_kernel;
+  if (fk == 0) {
+    // auto: the capped lookup-table kernel for capped calls; else the fastest
+    // int8 kernel whose worst-case ll error (nemo_host.h) stays within
+    // err_budget -- log2 fixed point (10), natural units (8), max offset (4)
+    // -- else the fp64 MFMA kernels
+    if (wincap) fk = 9;
+    else if (!i8cap) fk = 1;
+    else if (c.i8o_ok && c.i8l_ok && bnd(host::kFxLog2) <= c.err_budget) fk = 10;
+    else if (c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 8;
+    else if (!c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 4;
+    else fk = 2;
+  } else if (fk == 9 || fk == 15) {
+    if (!wincap) return -1;
+  } else if (fk == 2 || fk == 3) {
+    if (!(ll_only && c.fspad <= 64)) fk = 1;
+  } else if (fk >= 4) {
+    if (!i8cap) fk = 1;  // an int8 kernel asked for a call it cannot serve: chunked fp64
+    else if ((fk == 7 || fk == 8) && !c.i8o_ok) return -1;
+    else if (fk >= 10 && !(c.i8o_ok && c.i8l_ok)) return -1;
+  }
+  if (bound) {
+    const bool l2 = fk >= 10 && fk != 15, nat = fk >= 4 && fk <= 8;
+    *bound = l2 ? bnd(host::kFxLog2) : nat ? bnd(host::kFxNatural) : 0.0;
+  }
+  return fk;
+}
+
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st) {
   const int spad = c.fspad;
-  const int fk0 = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
   if (cap >= c.S - 1) cap = 0;  // every predecessor is within the cap: no cap (same bits)
-  const bool ll_only0 = !d_cs && !d_cells && !d_ow;
-  // capped ll-only calls: the banded lookup-table kernel (fact_kernel 9, its
-  // round-1 form with the row bits re-read from LDS 15; auto when staged),
-  // which derives its tables itself
-  const bool win = ll_only0 && c.win_ok && cap >= 1 && cap <= kWinMaxCap &&
-                   (c.fact_kernel == 0 || c.fact_kernel == 9 || c.fact_kernel == 15);
-  if ((c.fact_kernel == 9 || c.fact_kernel == 15) && !win) return hipErrorInvalidValue;
-  const bool i8_path = spad <= 64 && ((fk0 >= 4 && fk0 <= 8) || (fk0 >= 10 && fk0 <= 14) || fk0 == 16 || fk0 == 17) && ll_only0 && c.d_B8;
+  const bool ll_only = !d_cs && !d_cells && !d_ow;
+  // option fact_kernel: 0 auto (resolve_fact_kernel), 1 chunked, 2 / 3 f64
+  // pipelined with 4 / 8 waves per block, 4 / 5 int8 with 4 / 5 digit pairs,
+  // 6 int8 (4 pairs) with 8 waves, 7 / 8 int8 with the offset log-sum-exp
+  // (4 / 8 waves), 9 / 15 the capped lookup-table kernel (15: its round-1
+  // form), 10 / 11 the offset kernel in log2 fixed point (8 / 4 waves; 12: 16
+  // waves; 13: register-stationary; 14: 8 waves compiled for 6 waves per
+  // SIMD; 10 walks two effect tiles per iteration, 16 is the same kernel with
+  // one; 17: 10's walk in persistent blocks that prep the next evaluation
+  // during the walk)
+  const int fk = resolve_fact_kernel(c, cap, ll_only, nullptr);
+  if (fk < 0) return hipErrorInvalidValue;  // asked for a kernel the staged model does not support
+  const bool is_auto = c.fact_kernel == 0;
+  const bool win = fk == 9 || fk == 15;
+  const bool l2 = fk >= 10 && fk != 15;
+  const bool i8o = fk == 7 || fk == 8 || l2;
+  const bool i8 = fk >= 4 && fk <= 6;
+  const bool pipe = fk == 2 || fk == 3;
   hipError_t err = hipSuccess;
-  if (!i8_path && !win) {  // the int8 kernel derives its Delta digits itself
+  if (!i8 && !i8o && !win) {  // the int8 and lookup-table kernels derive their inputs themselves
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
@@ -551,37 +593,22 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     e1 = c.ev_pool[c.ev_used++];
     { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }
   }
-  // option fact_kernel: 0 auto (kAutoFactKernel for ll-only calls with
-  // S <= 64), 1 chunked, 2 / 3 f64 pipelined with 4 / 8 waves per block,
-  // 4 / 5 int8 with 4 / 5 digit pairs, 6 int8 (4 pairs) with 8 waves,
-  // 7 / 8 int8 with the offset log-sum-exp (4 / 8 waves), 10 / 11 the same in
-  // log2 fixed point (8 / 4 waves; 12: 16 waves; 13: register-stationary;
-  // 14: 8 waves compiled for 6 waves per SIMD; 10 walks two effect tiles per
-  // iteration, 16 is the same kernel with one; 17: 10's walk in persistent
-  // blocks that prep the next evaluation during the walk); auto prefers 10, then 8
-  const int fk = c.fact_kernel == 0 ? kAutoFactKernel : c.fact_kernel;
-  const bool ll_only = !d_cs && !d_cells && !d_ow;
-  const bool pipe = spad <= 64 && fk != 1 && fk < 4 && ll_only;
-  const bool i8 = spad <= 64 && ((fk >= 4 && fk <= 8) || (fk >= 10 && fk <= 14) || fk == 16 || fk == 17) && ll_only && c.d_B8;
   int np = 0;
   bool finalized = false;
-  const bool l2 = i8 && c.i8o_ok && c.i8l_ok && (fk >= 10 || c.fact_kernel == 0);
-  const bool i8o = i8 && c.i8o_ok && (fk == 7 || fk == 8 || c.fact_kernel == 0 || l2);
   if (win) {
-    err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized, c.fact_kernel == 15);
+    err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized, fk == 15);
   } else if (i8o) {
-    // 7 / 8: offset log-sum-exp with 4 / 8 waves per block, 10 / 11: log2
-    // fixed point with 8 / 4 (auto: 8)
-    // (10 and auto: 8 waves, two effect tiles per iteration; 16: one tile)
-    const int waves = fk == 17 ? -3 : fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : (fk == 12 ? 16 : (fk == 7 || fk == 11) ? 4 : (l2 ? -2 : 8));
+    // 7 / 8: offset log-sum-exp with 4 / 8 waves per block; 10 (auto's l2
+    // choice): 8 waves, two effect tiles per iteration; 11: 4 waves; 12: 16;
+    // 16: 8 waves, one tile per iteration
+    const int waves = fk == 17 ? -3 : fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : fk == 12 ? 16
+                    : (fk == 7 || fk == 11) ? 4 : fk == 10 ? -2 : 8;
     err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, l2, st, &np, &finalized);
-  } else if (i8 && fk <= 6) {
+  } else if (i8) {
     // auto: 4 waves per block for large batches, 8 (fewer splits) below
-    const int waves = fk == 6 ? 8 : (fk == 4 && c.fact_kernel == 0 && batch < 384 ? 8 : 4);
+    const int waves = fk == 6 ? 8 : (fk == 4 && is_auto && batch < 384 ? 8 : 4);
     err = launch_score_i8(c, batch, cap, d_pos, d_w01, d_ll, fk == 5 ? 5 : 4, waves, st, &np,
                           &finalized);
-  } else if (i8) {
-    return hipErrorInvalidValue;  // 7 / 8 / 10 / 11 asked for but the staging bounds do not hold
   } else if (pipe) {
     const bool w8 = fk == 3;
     switch (spad / 16) {

@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include "nemo_host.h"
+
 namespace nemo {
 
 constexpr int kWave = 64;
@@ -95,11 +97,14 @@ struct Ctx {
   double* d_wuw = nullptr;         // [S][2] U - U[S] of row i at D1 bit 0 / 1
   double* d_wnull = nullptr;       // [nwords] sum of U[S][e] over each 64-effect word
 
+  // worst-case |ll error| of the fixed-point kernels (nemo_host.h):
+  // fx_colsum[k] = sum_e min(colbits_e, k) over the staged D1 bits; auto takes
+  // a fixed-point kernel only while its bound stays within err_budget
+  std::vector<double> fx_colsum;
+  double err_budget = 1e-7;        // option "err_budget" (nemo_set_option_f64)
+
   // InverseMethod pair schedule (levels), cached per batch of orders
-  std::vector<int32_t> inv_pos;    // the orders the schedule was built for
-  std::vector<int32_t> inv_list;   // pair entries, level by level
-  std::vector<int> inv_level_off;  // level l = inv_list[off[l] .. off[l+1])
-  std::vector<int32_t> inv_skip;   // permissible pairs outside the lower triangle
+  host::InverseSchedule inv;
   int32_t* d_inv_list = nullptr;
   size_t inv_list_cap = 0;
 
@@ -308,5 +313,9 @@ hipError_t launch_inverse_level(Ctx& c, int n, const int32_t* d_list, const int3
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
                                  double* d_ow, hipStream_t st);
+// the fact_kernel value a factored call takes (the option, or what auto
+// resolves to for this cap / output set), with the worst-case |ll error| of
+// its fixed-point arithmetic (0 for the fp64 kernels); -1 if none applies
+int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound);
 
 }  // namespace nemo

@@ -34,6 +34,7 @@ _vp = C.c_void_p
 SIGNATURES = [
     ("nemo_last_error", C.c_char_p, []),
     ("nemo_version", C.c_int, []),
+    ("nemo_build_id", C.c_char_p, []),
     ("nemo_device_count", C.c_int, [_i32p]),
     ("nemo_ctx_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     ("nemo_ctx_destroy", None, [_vp]),
@@ -58,6 +59,9 @@ SIGNATURES = [
     ("nemo_inverse_sweep", C.c_int, [_vp, C.c_int, _i32p, _f64p, _f64p, _f64p, _i32p]),
     ("nemo_set_option", C.c_int, [_vp, C.c_char_p, C.c_int]),
     ("nemo_get_option", C.c_int, [_vp, C.c_char_p, _i32p]),
+    ("nemo_set_option_f64", C.c_int, [_vp, C.c_char_p, C.c_double]),
+    ("nemo_get_option_f64", C.c_int, [_vp, C.c_char_p, _f64p]),
+    ("nemo_score_kernel", C.c_int, [_vp, C.c_int, C.c_int, _i32p, _f64p]),
     ("nemo_timing_enable", C.c_int, [_vp, C.c_int]),
     ("nemo_timing_read", C.c_int, [_vp, _f64p, _i32p]),
 ]
@@ -112,6 +116,11 @@ def ptr(a, kind=_f64p):
     if a is None:
         return None
     return a.ctypes.data_as(kind)
+
+
+def build_id() -> str:
+    """The loaded library's build id (a hash of its sources and flags)."""
+    return load().nemo_build_id().decode()
 
 
 def device_count() -> int:

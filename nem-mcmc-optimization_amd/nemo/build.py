@@ -10,6 +10,7 @@ build is skipped when the library is newer than every source.
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -40,11 +41,31 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the engine needs ROCm's hipcc to build")
 
 
+def build_id(defines=()) -> str:
+    """Hash of every source and header the library is built from, the
+    compile flags and the target: the same tree gives the same id on any
+    host, so profiler records (profiles/*.json) can name the build they
+    measured."""
+    h = hashlib.sha256()
+    for p in sorted(_deps()):
+        h.update(os.path.relpath(p, REPO).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((ARCH, list(defines), _FLAGS)).encode())
+    return h.hexdigest()[:16]
+
+
+_FLAGS = ("-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function")
+
+
 def up_to_date() -> bool:
     if not os.path.exists(LIB):
         return False
     t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(p) <= t for p in _deps())
+    if not all(os.path.getmtime(p) <= t for p in _deps()):
+        return False
+    with open(LIB, "rb") as fh:  # built from these very sources (mtimes lie after a checkout)
+        return build_id().encode() in fh.read()
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
@@ -53,8 +74,8 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     target = out or LIB
     if not force and out is None and up_to_date():
         return LIB
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-             "-I", INCLUDE, "-I", SRC_DIR, *[f"-D{d}" for d in defines]]
+    flags = [f"--offload-arch={ARCH}", *_FLAGS, "-I", INCLUDE, "-I", SRC_DIR,
+             f'-DNEMO_BUILD_ID="{build_id(defines)}"', *[f"-D{d}" for d in defines]]
     jobs = max(1, min(len(_sources()), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
 
     def run(cmd):

@@ -327,3 +327,70 @@ def gather_best(best_scores, best_orders, device=None):
     out_s = np.concatenate([a[:c].cpu().numpy() for a, c in zip(all_s, counts)])
     out_o = np.concatenate([a[:c].cpu().numpy() for a, c in zip(all_o, counts)])
     return out_s, out_o
+
+
+def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_steps: int = 2, inv_workers=None,
+           device=None, cap: int = 0):
+    """BASELINE config C4 on the default process group (or alone without one):
+    ``n_chains`` independent chains of ``nem`` sharded over the ranks
+    (``shard``; chain c keeps seed 1234 + c and the reference's initial order
+    whatever the rank count), each rank's share run as ONE ``ChainBatch``
+    (the reference's per-chain state machines, nem_order_mcmc.py:257-310, one
+    fused device step per MCMC step), then ONE all-gather of every chain's
+    (best score, best order) -- the only collective.  The
+    ranks run ``warmup_steps`` untimed steps on a throw-away batch first.
+
+    Returns, on every rank, a dict: wall seconds of the timed run (max over
+    ranks, barrier before), chain-steps/s, the gathered scores and orders and
+    the global best."""
+    import hashlib
+    import time
+
+    from . import utils
+    from .invpool import InvPool, default_workers
+
+    world, rank = 1, 0
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            world, rank = dist.get_world_size(), dist.get_rank()
+    except ImportError:
+        dist = None
+    mine = shard(n_chains, rank, world)
+    order = utils.initial_order_guess(nem.observed_knockdown_mat)
+    seeds = [1234 + c for c in mine]
+    nw = default_workers() if inv_workers is None else int(inv_workers)
+    pool = InvPool(nem.num_s, len(mine), nw) if nw > 0 and len(mine) > 0 else None
+    try:
+        if warmup_steps > 0 and len(mine):
+            ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
+                       inv_pool=pool).run(warmup_steps)
+        cb = ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
+                        inv_pool=pool) if len(mine) else None
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        if cb is not None:
+            best, orders = cb.run(steps)
+        else:
+            best, orders = np.zeros(0), np.zeros((0, nem.num_s), dtype=np.int32)
+        if world > 1:
+            all_s, all_o = gather_best(best, orders, device=device)
+        else:
+            all_s, all_o = np.asarray(best, dtype=np.float64), np.asarray(orders)
+        wall = time.perf_counter() - t0
+    finally:
+        if pool is not None:
+            pool.close()
+    if world > 1:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64, device=device if device is not None else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    g = int(np.argmax(all_s))
+    return {"wall_s": wall, "chain_steps_per_s": n_chains * steps / wall, "ms_per_step": 1e3 * wall / steps,
+            "n_ranks": world, "chains_per_rank": len(mine), "inv_workers_per_rank": nw if pool else 0,
+            "n_gathered": int(len(all_s)), "best_score": float(all_s[g]), "best_chain": g,
+            "best_order": [int(v) for v in all_o[g]],
+            "scores_sha256": hashlib.sha256(np.ascontiguousarray(all_s, dtype=np.float64).tobytes()).hexdigest()[:16],
+            "scores": all_s, "orders": all_o}

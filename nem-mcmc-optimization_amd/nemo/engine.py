@@ -215,6 +215,23 @@ class Engine:
         check(_lib.load().nemo_get_option(self._ctx, name.encode(), C.byref(v)))
         return v.value
 
+    def set_option_f64(self, name: str, value: float):
+        check(_lib.load().nemo_set_option_f64(self._ctx, name.encode(), float(value)))
+
+    def get_option_f64(self, name: str) -> float:
+        v = C.c_double(0.0)
+        check(_lib.load().nemo_get_option_f64(self._ctx, name.encode(), C.byref(v)))
+        return v.value
+
+    def score_kernel(self, cap: int = 0, ll_only: bool = True):
+        """(fact_kernel, worst-case |ll error| bound) a factored score call
+        with this cap takes; fact_kernel -1 = the streaming kernel."""
+        fk = C.c_int32(0)
+        b = C.c_double(0.0)
+        check(_lib.load().nemo_score_kernel(self._ctx, int(cap), 1 if ll_only else 0, C.byref(fk),
+                                            C.byref(b)))
+        return fk.value, b.value
+
     @property
     def factored(self) -> bool:
         """True when the staged table has the NEM structure the MFMA kernel uses."""

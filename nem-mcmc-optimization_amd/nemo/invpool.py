@@ -21,6 +21,21 @@ import os
 import numpy as np
 
 
+def default_workers(local_world: int | None = None, cap: int = 8) -> int:
+    """Worker processes per rank so that the ranks of one node do not
+    oversubscribe its cores: the cores this process may run on, shared by
+    the node's ranks (LOCAL_WORLD_SIZE), minus one for the rank itself;
+    at least 1, at most ``cap`` (8 measured best for 128 chains on one GPU,
+    DESIGN.md 6)."""
+    if local_world is None:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cores = os.cpu_count() or 1
+    return max(1, min(cap, cores // max(1, local_world) - 1))
+
+
 def _worker(conn, names, maxb, s):
     from multiprocessing import shared_memory
     from scipy.linalg import get_lapack_funcs

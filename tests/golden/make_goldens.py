@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -97,13 +97,18 @@ def ref_eval(ref_mcmc, m, tables, perm, w_raw, cap=0):
 
 
 def capture_evals(ref_nem, ref_mcmc, ref_utils, gen, name, s, e, seed, cap, n_eval, keep_ow):
+    """n_eval evaluations with the inputs of tests/golden/eval_inputs.py
+    (k < 20: random orders and W ~ U(-3, 3); then saturated, all-0, all-1,
+    all-1/2 and mixed 0/1 weights, the identity and reversed orders)."""
+    sys.path.insert(0, HERE)
+    from eval_inputs import KINDS, eval_inputs
     net = gen.synthetic_network(s, e, seed)
     m = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, s, e)
     tables = m.get_score_tables(m.observed_knockdown_mat)
     perms, ws, lls, css = [], [], [], []
     ow0 = None
     for c in range(n_eval):
-        perm, _pos, w = gen.random_chain_inputs(s, c)
+        perm, w = eval_inputs(s, c)
         ll, cs, ow = ref_eval(ref_mcmc, m, tables, perm, w, cap)
         perms.append(perm)
         ws.append(w)
@@ -115,7 +120,8 @@ def capture_evals(ref_nem, ref_mcmc, ref_utils, gen, name, s, e, seed, cap, n_ev
     out = dict(S=s, E=e, seed=seed, cap=cap, A=m.A, B=m.B,
                D_packed=np.packbits(d, axis=None),
                U_sha256=hashlib.sha256(np.ascontiguousarray(m.U, dtype=np.float64).tobytes()).hexdigest(),
-               perm=np.array(perms), W=np.array(ws), ll=np.array(lls), cs=np.array(css))
+               perm=np.array(perms), W=np.array(ws), ll=np.array(lls), cs=np.array(css),
+               kind=np.array(KINDS[:n_eval]))
     if ow0 is not None:
         out["ow0"] = ow0
     if s <= 16:
@@ -334,6 +340,10 @@ def main():
     if "--only-methods" in sys.argv:
         capture_methods(ref_nem, ref_utils, gen)
         return
+    if "--only-evals" in sys.argv:
+        capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)
+        capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C5cap", 128, 5000, 0, 6, 32, False)
+        return
 
     # KAT from the reference's own test (tests/utils.tests.py:11-27): data only.
     s_mat = np.array([[0, 1, 1, 0, 1, 0], [0, 0, 1, 0, 1, 0], [0, 0, 0, 0, 1, 0],
@@ -371,8 +381,8 @@ def main():
 
     # synthetic evals: C2, C3, C5 (cap 6, reference fp64)
     capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C2", 16, 500, 0, 0, 8, True)
-    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 4, True)
-    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C5cap", 128, 5000, 0, 6, 3, False)
+    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)
+    capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C5cap", 128, 5000, 0, 6, 32, False)
 
     # C2 trajectory, 20 steps (default swap_prob 0.95, gamma = 2S/E)
     net = gen.synthetic_network(16, 500, 0)

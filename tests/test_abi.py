@@ -13,7 +13,7 @@ from conftest import REPO
 def _declared():
     text = open(os.path.join(REPO, "include", "nemo.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(nemo_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(nemo_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.fixture(scope="module")

@@ -21,11 +21,43 @@ def test_algorithmic_figures():
     assert bench.n_pairs(128, 6) == 747
 
 
-def test_profile_records_for_the_headline_kernel():
-    t = bench.load_traffic("C3:i8l:b2048")
-    assert t and t["bytes_per_launch"] > 6e7  # the w01 input, 2048 x 32 KB
-    v = bench.load_valu_bound("C3:i8l:b2048")
-    assert v and 0.0 < v["valu_busy"] < 1.0 and 0.0 < v["lds_busy"] < 1.0
+def test_profile_records_are_tied_to_the_build(tmp_path, monkeypatch):
+    # a PMC record names the libnemo.so build it measured; another build's
+    # record is stale and never attached to a fresh timing
+    import json
+    (tmp_path / "profiles").mkdir()
+    rec = {"C3:i8l:b2048": {"build_id": "aaaa", "bytes_per_launch": 6.66e7}}
+    (tmp_path / "profiles" / "traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    assert bench.load_record("traffic.json", "C3:i8l:b2048", "aaaa")["bytes_per_launch"] == 6.66e7
+    assert bench.load_record("traffic.json", "C3:i8l:b2048", "bbbb") is None
+    assert bench.load_record("valu.json", "C3:i8l:b2048", "aaaa") is None
+
+
+def test_roofline_is_a_hardware_fraction(monkeypatch):
+    # with the PMC record of the build: bound = VALU issue, frac <= 1 against
+    # the max-clock issue peak, the int8 matrix cores and HBM beside it <= 1
+    valu = {"build_id": "x", "SQ_ACTIVE_INST_VALU": 68724736.0, "SQ_LDS_IDX_ACTIVE": 51627709.0,
+            "SQ_LDS_BANK_CONFLICT": 21046973.0, "valu_busy": 0.766, "mfma_busy": 0.322}
+    traffic = {"build_id": "x", "bytes_per_launch": 66.6e6}
+    monkeypatch.setattr(bench, "load_record", lambda name, key, bid: valu if name == "valu.json" else traffic)
+    r = bench.score_roofline("C3", 64, 2000, 0, 2048, 10, 0.1466, 0.149, "x")
+    assert r["bound"] == "valu" and 0.5 < r["frac"] <= 1.0
+    assert abs(r["frac"] - 4 * 68724736.0 / 0.1466e-3 / (1024 * 2.4e9)) < 1e-12
+    for k, v in r["secondary"].items():
+        assert 0.0 < v["frac"] <= 1.0, k
+    assert 0.25 < r["secondary"]["int8_mfma"]["frac"] < 0.4
+    assert r["fp64_equivalent"]["vs_f64_mfma_peak"] > 1.0   # the note, not the headline
+    assert r["traffic"] == 66.6e6 / 2048
+    # without a record of this build: the live int8 matrix-core fraction
+    monkeypatch.setattr(bench, "load_record", lambda name, key, bid: None)
+    r = bench.score_roofline("C3", 64, 2000, 0, 2048, 10, 0.1466, 0.149, "y")
+    assert r["bound"] == "mfma" and r["frac"] <= 1.0 and r["traffic"] is None
+
+
+def test_kernel_tags():
+    assert bench.kernel_tag(10) == "i8l" and bench.kernel_tag(8) == "i8o" and bench.kernel_tag(4) == "i8"
+    assert bench.kernel_tag(9) == "win2" and bench.kernel_tag(2) == "pipe" and bench.kernel_tag(1) == "factored"
 
 
 @pytest.mark.timeout(180)

@@ -168,7 +168,8 @@ def test_local_opt_vs_scipy_records(name, prod):
     xs, fs, nit, nfev, st = eng.local_opt(z["c"], z["anc"], z["x0"])
     assert np.all(st <= 1)
     same = (nit == z["nit"]) & (nfev == z["nfev"])
-    assert same.mean() >= 0.97
+    # every recorded problem follows scipy's iteration path
+    assert same.all(), f"{int((~same).sum())} of {same.size} problems left scipy's (nit, nfev) path"
     rel = np.abs(xs - z["xstar"]) / np.maximum(1, np.abs(z["xstar"]))
     assert np.max(rel[same]) <= 1e-3
     assert np.array_equal(np.sign(xs), np.sign(z["xstar"]))
@@ -658,6 +659,11 @@ def test_queued_fused_step_equals_direct_call():
         for x, y in zip(c.result(raise_on_fail=False), d):
             assert np.array_equal(x, y)
     assert _lib.load().nemo_optimal_weights_end(eng._ctx) == _lib.NEMO_ERR_STATE
-    # a queued call still running when the engine closes is waited for
-    calls[0].begin()
+    # calls still queued when the engine closes run to completion first: their
+    # output buffers hold the direct call's results although no _end collects them
+    for c in calls:
+        c.w_new[:] = np.nan
+        c.begin()
     eng.close()
+    for c, d in zip(calls, direct):
+        assert np.array_equal(c.w_new, d[0]) and np.array_equal(c.ll1, d[1])

@@ -11,6 +11,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
+from nemo.build import build_id  # noqa: E402  (the record names the build it measured)
+
 
 def per_kernel(path, counter):
     """Mean per dispatch (rows of one dispatch summed), the first (cold)
@@ -43,7 +46,8 @@ def main():
         key = prefix.replace("{kind}", kind)
         data[key] = {"bytes_per_launch": 2 * 1024 * f[kind] + 1024 * w.get(kind, 0.0),
                      "fetch_size_kib": f[kind], "write_size_kib": w.get(kind, 0.0),
-                     "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE, KiB"}
+                     "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE, KiB",
+                     "build_id": build_id()}
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data, indent=1))
 

@@ -15,6 +15,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
+from nemo.build import build_id  # noqa: E402  (the record names the build it measured)
+
 TAGS = (("score_window2_kernel", "win2"), ("score_window_kernel", "win"), ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
         ("score_factored_kernel", "factored"), ("score_kernel", "stream"))
 
@@ -45,7 +48,8 @@ def main():
     for kind, d in agg.items():
         key = prefix.replace("{kind}", kind)
         # passes of the same kernel merge: counters of earlier passes are kept
-        m = {k: v for k, v in data.get(key, {}).items() if k.isupper()}
+        old = data.get(key, {})
+        m = {k: v for k, v in old.items() if k.isupper()} if old.get("build_id") == build_id() else {}
         m.update({k: sum(v) / len(v) for k, v in d.items()})
         rec = {k: m[k] for k in sorted(m)}
         if "SQ_ACTIVE_INST_VALU" in m and "GRBM_GUI_ACTIVE" in m:
@@ -61,6 +65,7 @@ def main():
                           "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / the same; mfma_coexec_frac = "
                           "SQ_VALU_MFMA_COEXEC_CYCLES / SQ_VALU_MFMA_BUSY_CYCLES (MFMA cycles with a VALU "
                           "issue beside them); lds_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE / 8)")
+        rec["build_id"] = build_id()
         data[key] = rec
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data, indent=1))
