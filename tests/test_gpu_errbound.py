@@ -37,7 +37,9 @@ def test_c3_auto_takes_log2_kernel_within_budget():
     assert eng.get_option_f64("err_budget") == 1e-7
     assert fk == 10 and 0.0 < bound <= 1e-7
     assert bound == eng.get_option_f64("i8l_bound")
-    assert eng.get_option_f64("i8o_bound") < bound / 1000
+    # the 8-slice kernel carries 2^-45 per entry at this model's scale (c = 4)
+    # against the log2 kernel's 2^-39 ln 2: ~45x tighter
+    assert eng.get_option_f64("i8o_bound") < bound / 40
     pos = np.array([_pos(p) for p in z["perm"]])
     w01 = expit(z["W"])
     # every kernel within its own bound of the reference's ll (plus the fp64

@@ -200,7 +200,12 @@ def test_fused_step_vs_oracle_c3(c3_model):
     mask = smp._mask
     assert np.array_equal(smp.parent_weights[~mask], ora.w[~mask])
     dw = np.abs(smp.parent_weights[mask] - ora.w[mask])
-    assert np.mean(dw <= 1e-6) >= 0.97 and np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
+    # 16 of the 2016 optima differ from scipy's by more than 1e-6 (max 8.5e-3,
+    # tools/parity_stats.py): the order weights differ from numpy's in the
+    # last bits and the forward-difference gradient (h = 1e-8) amplifies that
+    # into another line-search path; every binarised weight is the same
+    assert int((dw > 1e-6).sum()) <= 16 and dw.max() <= 1e-2
+    assert np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
     assert abs(got_dag - ref_dag) <= LL_TOL
 
 
@@ -644,10 +649,11 @@ def test_queued_fused_step_equals_direct_call():
     m = generator.synthetic_nem(64, 2000, 3)
     eng = Engine.for_nem(m)
     rng = np.random.default_rng(21)
-    calls, direct = [], []
+    calls, direct, w_orig = [], [], []
     for n in (3, 5):
         pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
         w = rng.uniform(-3, 3, (n, 64, 64))
+        w_orig.append(w)
         anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
         direct.append(eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False))
         calls.append(eng.bind_optimal_weights(pos, expit(w), anc, w, SIG0, SIG1))
@@ -661,9 +667,14 @@ def test_queued_fused_step_equals_direct_call():
     assert _lib.load().nemo_optimal_weights_end(eng._ctx) == _lib.NEMO_ERR_STATE
     # calls still queued when the engine closes run to completion first: their
     # output buffers hold the direct call's results although no _end collects them
-    for c in calls:
-        c.w_new[:] = np.nan
-        c.begin()
+    again = []
+    for c, w in zip(calls, w_orig):
+        pos, w01, anc = c._keep
+        a = eng.bind_optimal_weights(pos, w01, anc, w, SIG0, SIG1)
+        a.ll1[:] = np.nan
+        a.lld[:] = np.nan
+        a.begin()
+        again.append(a)
     eng.close()
-    for c, d in zip(calls, direct):
-        assert np.array_equal(c.w_new, d[0]) and np.array_equal(c.ll1, d[1])
+    for a, d in zip(again, direct):
+        assert np.array_equal(a.w_new, d[0]) and np.array_equal(a.ll1, d[1]) and np.array_equal(a.lld, d[2])
