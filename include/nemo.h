@@ -213,7 +213,11 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                and rides in the contraction (no U reads)
  *   "i8o_nodiag" 1 = keep the U reads even when 2 is available (testing)
  *   "i8l"        (get only) 1 if the log2 fixed-point offset kernel is staged
- *                (i8o = 2 and |Delta|, |U - U[S]| / ln 2 within its digit range) */
+ *                (i8o = 2 and |Delta|, |U - U[S]| / ln 2 within its digit range)
+ *   "local_split" 2 = run each local optimum of a fused step on a 4-wave
+ *                block (the objective's products split over the waves; same
+ *                bits; measured slower for one chain, so 0 = auto never
+ *                takes it), 1 = never */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

@@ -877,6 +877,11 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.i8o_nodiag = value != 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "local_split") == 0) {
+    if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "local_split=%d not in {0,1,2}", value);
+    ctx->c.local_split = value;
+    return NEMO_OK;
+  }
   if (strcmp(name, "score_path") == 0) {
     if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "score_path=%d not in {0,1,2}", value);
     ctx->c.score_path = value;
@@ -897,6 +902,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
   else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
   else if (strcmp(name, "i8l") == 0) *value = c.i8l_ok ? 1 : 0;
+  else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);

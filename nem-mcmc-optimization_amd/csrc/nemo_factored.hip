@@ -469,10 +469,9 @@ __global__ __launch_bounds__(WAVES * kWave, 2) void score_factored_pipe_kernel(
   if (lane == 0) *part_out = v;
 }
 
-template <int NR>
-hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_cs, double* d_cells,
+template <int NR, int WAVES>
+hipError_t launch_fact_w(Ctx& c, int batch, int cap, double* d_cs, double* d_cells,
                          double* d_ow, hipStream_t st, int* nparts) {
-  constexpr int WAVES = kFactWaves;
   constexpr int SPAD = NR * 16;
   constexpr int KC = SPAD < 64 ? SPAD : 64;
   constexpr int COLS = WAVES * 16;
@@ -484,6 +483,18 @@ hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_cs, double* d_cel
       c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap);
   *nparts = nt * WAVES;
   return hipGetLastError();
+}
+
+// partial t of an evaluation is its 16-effect tile t's sum whatever WAVES
+// is (sum_partials adds the zero padding of the last block exactly), so any
+// WAVES gives the same bits.  Tried: 2 waves (32 effects) per block for the
+// fused step of one chain (63 blocks instead of 16): 23 against 18 us per
+// launch -- each block stages the whole Delta (32 KB) with a quarter of the
+// threads -- so every batch takes 8 waves per block.
+template <int NR>
+hipError_t launch_fact_t(Ctx& c, int batch, int cap, double* d_cs, double* d_cells,
+                         double* d_ow, hipStream_t st, int* nparts) {
+  return launch_fact_w<NR, kFactWaves>(c, batch, cap, d_cs, d_cells, d_ow, st, nparts);
 }
 
 template <int NR, int WAVES>

@@ -31,6 +31,7 @@ struct Ctx {
   int xcd_remap = 1;               // option "xcd_remap": XCD-aware block order
   double table_absmax = 0.0;       // max |T| over off-diagonal rows
   bool local_prod = true;          // option "local_prod": local optima sum logs as one log of a product
+  int local_split = 0;             // option "local_split": 0 auto, 1 never, 2 always (4 waves per problem)
   void* d_eT = nullptr;            // exp(T) [S][S][E] (dtype)
   void* d_U = nullptr;             // U [S+1][E] (dtype)
 

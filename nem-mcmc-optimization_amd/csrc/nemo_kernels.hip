@@ -90,52 +90,56 @@ __global__ void exp_table_kernel(size_t n, const double* __restrict__ t64, TT* _
 // prep: per evaluation, per child i, the permissible parents in pi order
 // (nem_order_mcmc.py:62-65; with cap, the last `cap` of them) and their
 // weights; plus the flat (child, list index) pair list for the local optima.
-// grid = batch, block = S rounded up to 64 (S <= 256).
+// grid = batch * ceil(S / 4), block = 256: one wave per child, one lane per
+// list slot (so a chain's prep is ceil(S / 4) blocks, not one serial loop per
+// child); every block rebuilds the evaluation's order and the prefix sums of
+// the list lengths in LDS (S <= 256).
 // ---------------------------------------------------------------------------
-__global__ void prep_kernel(int S, int cap, const int32_t* __restrict__ pos,
-                            const double* __restrict__ w01, int32_t* __restrict__ rows,
-                            double* __restrict__ sw, int32_t* __restrict__ cnt,
-                            int32_t* __restrict__ pairs) {
+__global__ __launch_bounds__(256) void prep_kernel(int S, int cap, const int32_t* __restrict__ pos,
+                                                   const double* __restrict__ w01, int32_t* __restrict__ rows,
+                                                   double* __restrict__ sw, int32_t* __restrict__ cnt,
+                                                   int32_t* __restrict__ pairs) {
   __shared__ int perm[kMaxS];
   __shared__ int scan[kMaxS];
-  const int b = blockIdx.x;
-  const int i = threadIdx.x;
-  if (i < S) perm[i] = 0;
+  const int nblk = (S + 3) / 4;
+  const int b = blockIdx.x / nblk;
+  const int i = (blockIdx.x - b * nblk) * 4 + (int)(threadIdx.x / kWave);  // this wave's child
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int32_t* pb = pos + (size_t)b * S;
+  if (tid < S) perm[tid] = 0;
   __syncthreads();
-  int pi = 0;
-  if (i < S) {
-    pi = pos[(size_t)b * S + i];
-    pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);  // malformed input must not fault
-    perm[pi] = i;
+  if (tid < S) {
+    int p = pb[tid];
+    p = p < 0 ? 0 : (p >= S ? S - 1 : p);  // malformed input must not fault
+    perm[p] = tid;
+    const int lo = (cap > 0 && p > cap) ? p - cap : 0;
+    scan[tid] = p - lo;  // list length of child tid
   }
   __syncthreads();
-  int lo = 0, n = 0;
-  if (i < S) {
-    lo = (cap > 0 && pi > cap) ? pi - cap : 0;
-    n = pi - lo;
-    int32_t* r = rows + ((size_t)b * S + i) * S;
-    double* w = sw + ((size_t)b * S + i) * S;
-    const double* wr = w01 + ((size_t)b * S + i) * S;
-    for (int t = 0; t < n; ++t) {
-      const int j = perm[lo + t];
-      r[t] = j;
-      w[t] = wr[j];
+  if (pairs != nullptr) {  // inclusive prefix sums of the lengths (Hillis-Steele)
+    for (int o = 1; o < S; o <<= 1) {
+      const int v = (tid < S && tid >= o) ? scan[tid - o] : 0;
+      __syncthreads();
+      if (tid < S) scan[tid] += v;
+      __syncthreads();
     }
-    cnt[(size_t)b * S + i] = n;
   }
-  if (pairs == nullptr) return;
-  scan[i] = (i < S) ? n : 0;
-  __syncthreads();
-  for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-    const int v = (i >= o) ? scan[i - o] : 0;
-    __syncthreads();
-    scan[i] += v;
-    __syncthreads();
+  if (i >= S) return;  // uniform per wave
+  int pi = pb[i];
+  pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);
+  const int lo = (cap > 0 && pi > cap) ? pi - cap : 0;
+  const int n = pi - lo;
+  int32_t* r = rows + ((size_t)b * S + i) * S;
+  double* w = sw + ((size_t)b * S + i) * S;
+  const double* wr = w01 + ((size_t)b * S + i) * S;
+  int32_t* pr = pairs ? pairs + (size_t)b * S * S + (scan[i] - n) : nullptr;
+  for (int t = lane; t < n; t += kWave) {
+    const int j = perm[lo + t];
+    r[t] = j;
+    w[t] = wr[j];
+    if (pr) pr[t] = (i << 16) | t;
   }
-  if (i < S) {
-    int32_t* pr = pairs + (size_t)b * S * S + (scan[i] - n);
-    for (int t = 0; t < n; ++t) pr[t] = (i << 16) | t;
-  }
+  if (lane == 0) cnt[(size_t)b * S + i] = n;
 }
 
 // ---------------------------------------------------------------------------
@@ -391,9 +395,9 @@ __device__ __forceinline__ double local_c(double lv, double owk, double s) {
   return a / b;
 }
 
-// PROD: sum_e log(c_e e + 1) as the log of a product -- per lane, the
-// factors multiplied with a frexp renormalisation every 8 (the caller
-// guarantees 8 factors stay in range: |T| <= 40 makes each factor lie in
+// PROD: sum_e log(c_e e + 1) as the log of a product -- per lane, chains of
+// 4 factors renormalised by frexp and combined in a fixed tree (the caller
+// guarantees the factors stay in range: |T| <= 40 makes each factor lie in
 // [e^-80, e^80]) and ONE log per lane, instead of a log per element.  Every
 // factor is > 0 for weights in [0, 1] (1 + e a / b = (b + e a) / b with b =
 // 1 + s (lv - 1)(1 - ow) > 0), as the reference's log needs too.
@@ -410,24 +414,42 @@ struct LocalObjective {
     if constexpr (PROD) {
       constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;
       constexpr double kLn2Lo = 5.4956039718945254e-14;
-      double m0 = 1.0, m1 = 1.0;
+      // NC independent chains of 4 factors (chain u: elements 4u .. 4u + 3 of
+      // the lane), each renormalised once by frexp, then the mantissas
+      // multiplied in a fixed pairwise tree: the dependent chain of an
+      // f-evaluation (the line search's serial path) is 4 + log2(NC) products
+      // instead of NPL.  4 factors stay in [e^-320, e^320] for |T| <= 40, a
+      // product of <= 32 mantissas in [0.5, 1) stays normal.
+      constexpr int NC = NPL / 4;
+      double m0[NC], m1[NC];
       int k0 = 0, k1 = 0;
 #pragma unroll
-      for (int q = 0; q < NPL; q += 8) {
+      for (int u = 0; u < NC; ++u) {
+        // one FMA per factor (the reference rounds c e and + 1 separately;
+        // the product form already departs from its sum of logs)
+        double a0 = fma(c[4 * u], e0, 1.0), a1 = fma(c[4 * u], e1, 1.0);
 #pragma unroll
-        for (int u = 0; u < 8 && q + u < NPL; ++u) {  // NPL may be 4
-          // one FMA per factor (the reference rounds c e and + 1 separately;
-          // the product form already departs from its sum of logs)
-          m0 *= fma(c[q + u], e0, 1.0);
-          m1 *= fma(c[q + u], e1, 1.0);
+        for (int v = 1; v < 4; ++v) {
+          a0 *= fma(c[4 * u + v], e0, 1.0);
+          a1 *= fma(c[4 * u + v], e1, 1.0);
         }
-        k0 += __builtin_amdgcn_frexp_exp(m0);
-        m0 = __builtin_amdgcn_frexp_mant(m0);
-        k1 += __builtin_amdgcn_frexp_exp(m1);
-        m1 = __builtin_amdgcn_frexp_mant(m1);
+        k0 += __builtin_amdgcn_frexp_exp(a0);
+        m0[u] = __builtin_amdgcn_frexp_mant(a0);
+        k1 += __builtin_amdgcn_frexp_exp(a1);
+        m1[u] = __builtin_amdgcn_frexp_mant(a1);
       }
-      p0 = fma((double)k0, kLn2Hi, log_fast(m0, ltab)) + (double)k0 * kLn2Lo;
-      p1 = fma((double)k1, kLn2Hi, log_fast(m1, ltab)) + (double)k1 * kLn2Lo;
+#pragma unroll
+      for (int wd = 1; wd < NC; wd *= 2)
+#pragma unroll
+        for (int u = 0; u + wd < NC; u += 2 * wd) {
+          m0[u] *= m0[u + wd];
+          m1[u] *= m1[u + wd];
+        }
+      k0 += __builtin_amdgcn_frexp_exp(m0[0]);
+      k1 += __builtin_amdgcn_frexp_exp(m1[0]);
+      const double r0 = __builtin_amdgcn_frexp_mant(m0[0]), r1 = __builtin_amdgcn_frexp_mant(m1[0]);
+      p0 = fma((double)k0, kLn2Hi, log_fast(r0, ltab)) + (double)k0 * kLn2Lo;
+      p1 = fma((double)k1, kLn2Hi, log_fast(r1, ltab)) + (double)k1 * kLn2Lo;
     } else {
 #pragma unroll
       for (int q = 0; q < NPL; ++q) {
@@ -458,6 +480,16 @@ __device__ __forceinline__ int32_t pack_info(const LbfgsResult& r) {
 #define NEMO_LOCAL_OPT_WAVES 3
 #endif
 constexpr int kLocalOptWavesPerSimd = NEMO_LOCAL_OPT_WAVES;
+// at most this many (chain, pair) problems take the 4-wave split form under
+// auto.  0: measured slower for one chain at C3 (84 against 75-79 us per
+// launch, tools/step_probe.py): a lone wave's f-evaluation is bound by its
+// dependent chain (expit, log, wave sums, the line-search logic), not by the
+// products the split divides, and the split adds a barrier and an LDS round
+// trip per f-evaluation.  Kept for A/B (option local_split = 2; same bits).
+#ifndef NEMO_LOCAL_SPLIT_MAX
+#define NEMO_LOCAL_SPLIT_MAX 0
+#endif
+constexpr int kLocalSplitMax = NEMO_LOCAL_SPLIT_MAX;
 
 // pairs of the fused per-step scorer.  grid covers nchains * npairs waves.
 template <typename TT, int NPL, bool PROD>
@@ -493,6 +525,134 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
   obj.anc = anc[idx];
   const LbfgsResult r = lbfgsb1_minimize(obj, s);
   if (lane == 0) {
+    const double wx = expit_d(r.x);
+    wnew[idx] = wx;
+    wdag[idx] = (wx > 0.5) ? sig1 : sig0;
+    if (info) info[idx] = pack_info(r);
+  }
+}
+
+// The same objective with one problem's effects split over the 4 waves of a
+// block (wave w: the lane's elements 8w .. 8w + 7 of LocalObjective's NPL =
+// 32, i.e. its chains 2w, 2w + 1; NPL = 16 / 64: one / four chains per
+// wave).  Each wave multiplies its chains and the first tree levels, posts
+// the product and exponent sum per lane to LDS, and after ONE barrier every
+// wave finishes the tree over the four posts in LocalObjective's order
+// ((w0 w1)(w2 w3)), then the log and the wave sum: every bit of f equals
+// LocalObjective's, in all four waves, so the four run the same L-BFGS-B
+// control flow.  For few problems (one chain's step) the serial line search
+// of the slowest pair sets the kernel's time, and a wave issues the whole
+// objective (~430 instructions per f-evaluation at NPL = 32) alone: split,
+// each wave issues a quarter of the products.  Posts are double-buffered, so
+// one barrier per f-evaluation suffices.
+template <int NPL>
+struct SplitObjective {
+  static constexpr int NC = NPL / 4;  // chains of LocalObjective
+  static constexpr int L = NC / 4;    // chains per wave (a power of 2)
+  static_assert(L == 1 || L == 2 || L == 4, "split objective: NPL in {16, 32, 64}");
+  double c[4 * L];                    // this lane's elements 4 L w .. 4 L w + 4 L - 1
+  double anc;
+  const double2* ltab;
+  double2* post;                      // LDS [2 buffers][4 waves][64 lanes] (m(x0), m(x1))
+  int2* kpost;                        // LDS [2][4][64] (k(x0), k(x1))
+  int w, lane;
+  mutable int par = 0;
+  __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
+#pragma clang fp contract(off)
+    constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;
+    constexpr double kLn2Lo = 5.4956039718945254e-14;
+    const double e0 = expit_d(x0);
+    const double e1 = expit_d(x1);
+    double m0[L], m1[L];
+    int k0 = 0, k1 = 0;
+#pragma unroll
+    for (int u = 0; u < L; ++u) {
+      double a0 = fma(c[4 * u], e0, 1.0), a1 = fma(c[4 * u], e1, 1.0);
+#pragma unroll
+      for (int v = 1; v < 4; ++v) {
+        a0 *= fma(c[4 * u + v], e0, 1.0);
+        a1 *= fma(c[4 * u + v], e1, 1.0);
+      }
+      k0 += __builtin_amdgcn_frexp_exp(a0);
+      m0[u] = __builtin_amdgcn_frexp_mant(a0);
+      k1 += __builtin_amdgcn_frexp_exp(a1);
+      m1[u] = __builtin_amdgcn_frexp_mant(a1);
+    }
+#pragma unroll
+    for (int wd = 1; wd < L; wd *= 2)
+#pragma unroll
+      for (int u = 0; u + wd < L; u += 2 * wd) {
+        m0[u] *= m0[u + wd];
+        m1[u] *= m1[u + wd];
+      }
+    const int slot = (par * 4 + w) * kWave + lane;
+    post[slot] = double2{m0[0], m1[0]};
+    kpost[slot] = int2{k0, k1};
+    __syncthreads();
+    const int base = par * 4 * kWave + lane;
+    const double2 q0 = post[base], q1 = post[base + kWave], q2 = post[base + 2 * kWave],
+                  q3 = post[base + 3 * kWave];
+    const int2 j0 = kpost[base], j1 = kpost[base + kWave], j2 = kpost[base + 2 * kWave],
+               j3 = kpost[base + 3 * kWave];
+    par ^= 1;
+    double r0 = (q0.x * q1.x) * (q2.x * q3.x);
+    double r1 = (q0.y * q1.y) * (q2.y * q3.y);
+    int kk0 = j0.x + j1.x + j2.x + j3.x, kk1 = j0.y + j1.y + j2.y + j3.y;
+    kk0 += __builtin_amdgcn_frexp_exp(r0);
+    kk1 += __builtin_amdgcn_frexp_exp(r1);
+    r0 = __builtin_amdgcn_frexp_mant(r0);
+    r1 = __builtin_amdgcn_frexp_mant(r1);
+    double p0 = fma((double)kk0, kLn2Hi, log_fast(r0, ltab)) + (double)kk0 * kLn2Lo;
+    double p1 = fma((double)kk1, kLn2Hi, log_fast(r1, ltab)) + (double)kk1 * kLn2Lo;
+    p0 = wsum_dpp(p0);
+    p1 = wsum_dpp(p1);
+    f0 = (-p0 + fabs(e0 - anc)) + e0 * (1.0 - e0);
+    f1 = (-p1 + fabs(e1 - anc)) + e1 * (1.0 - e1);
+  }
+};
+
+// local_opt_pairs_kernel with one (chain, pair) per 4-wave block
+// (SplitObjective): the same results bit for bit.  grid = nchains * npairs.
+template <typename TT, int NPL>
+__global__ __launch_bounds__(256) void local_opt_pairs_split_kernel(
+    int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
+    const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
+    const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
+    double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
+    int32_t* __restrict__ info) {
+  __shared__ double2 ltab[128];
+  __shared__ double2 post[2 * 4 * kWave];
+  __shared__ int2 kpost[2 * 4 * kWave];
+  fill_log_table(ltab, threadIdx.x, blockDim.x);
+  __syncthreads();
+  const int gp = blockIdx.x;  // one problem per block
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  const int b = gp / npairs;
+  const int n = gp - b * npairs;
+  const int pk = pairs[(size_t)b * S * S + n];
+  const int i = pk >> 16;
+  const int t = pk & 0xffff;
+  const int k = rows[((size_t)b * S + i) * S + t];
+  const size_t idx = ((size_t)b * S + i) * S + k;
+  const double s = w01[idx];
+  const TT* tv = eT + ((size_t)i * S + k) * E;
+  const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
+  using Obj = SplitObjective<NPL>;
+  Obj obj;
+  obj.ltab = ltab;
+  obj.post = post;
+  obj.kpost = kpost;
+  obj.w = w;
+  obj.lane = lane;
+#pragma unroll
+  for (int q = 0; q < 4 * Obj::L; ++q) {
+    const int e = (4 * Obj::L * w + q) * kWave + lane;
+    obj.c[q] = (e < E) ? local_c((double)tv[e], owk[e], s) : 0.0;  // padding: log(1) = 0
+  }
+  obj.anc = anc[idx];
+  const LbfgsResult r = lbfgsb1_minimize(obj, s);
+  if (w == 0 && lane == 0) {
     const double wx = expit_d(r.x);
     wnew[idx] = wx;
     wdag[idx] = (wx > 0.5) ? sig1 : sig0;
@@ -559,8 +719,7 @@ hipError_t launch_exp_table(Ctx& c, const double* d_T64, hipStream_t st) {
 hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                        int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
                        hipStream_t st) {
-  const int threads = ((c.S + kWave - 1) / kWave) * kWave;
-  prep_kernel<<<batch, threads, 0, st>>>(c.S, cap, d_pos, d_w01, d_rows, d_sw, d_cnt, d_pairs);
+  prep_kernel<<<batch * ((c.S + 3) / 4), 256, 0, st>>>(c.S, cap, d_pos, d_w01, d_rows, d_sw, d_cnt, d_pairs);
   return hipGetLastError();
 }
 
@@ -683,8 +842,26 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
   const size_t waves = (size_t)nchains * npairs;
   const int blocks = (int)((waves + 3) / 4);
   const TT* eT = (const TT*)c.d_eT;
-  // the product form needs every 8 factors in range (LocalObjective)
+  // the product form needs every 4 factors in range (LocalObjective)
   const bool prod = c.local_prod && c.table_absmax <= 40.0;
+  // few problems: one block of 4 waves per problem (SplitObjective, same
+  // bits); option "local_split": 0 auto, 1 never, 2 always (where it applies)
+  const int npl = npl_for(c.E);
+  const bool splittable = prod && (npl == 16 || npl == 32 || npl == 64);
+  const bool split = splittable && (c.local_split == 2 || (c.local_split == 0 && waves <= (size_t)kLocalSplitMax));
+  if (split) {
+    const int nb = (int)waves;
+    if (npl == 16)
+      local_opt_pairs_split_kernel<TT, 16><<<nb, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                              d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+    else if (npl == 32)
+      local_opt_pairs_split_kernel<TT, 32><<<nb, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                              d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+    else
+      local_opt_pairs_split_kernel<TT, 64><<<nb, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                              d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+    return hipGetLastError();
+  }
 #define NEMO_LP(NPL)                                                                            \
   if (prod)                                                                                     \
     local_opt_pairs_kernel<TT, NPL, true><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, \
