@@ -142,7 +142,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_step};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_step, c.d_nullsum_w};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (c.h_stage) (void)hipHostFree(c.h_stage);
@@ -266,30 +266,34 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     HIPCHK(hipMemcpy(c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
-    // int8 variant (S <= 64): per-model fixed-point scale and the D1 bytes in
-    // v_mfma_i32_16x16x64_i8 B-fragment order: tile t, lane l (effect
-    // 16t + (l & 15), parents 16 (l >> 4) .. + 15), byte j = parent 16 (l >> 4) + j
+    // int8 variants (S <= 128): per-model fixed-point scale and the D1 bytes in
+    // v_mfma_i32_16x16x64_i8 B-fragment order: K half h (parents 64 h .. 64 h
+    // + 63; one half for S <= 64, two for S <= 128), tile t, lane l (effect
+    // 16t + (l & 15), parents 64 h + 16 (l >> 4) .. + 15), byte j = parent
+    // 64 h + 16 (l >> 4) + j
     if (c.d_B8) HIPCHK(hipFree(c.d_B8));
     c.d_B8 = nullptr;
-    if (S <= 64) {
+    if (S <= 128) {
       double dmax = 0.0;
       for (size_t j = 0; j < S; ++j) dmax = std::max(dmax, fabs(log(ehi[j]) - log(elo[j])));
       int ex = 0;
       if (dmax > 0.0) frexp(dmax * (1.0 + 1e-9), &ex);  // dmax * (1 + 1e-9) <= 2^ex
       c.i8_cexp = dmax > 0.0 ? ex + 1 : 0;              // |Delta| <= 2^(c - 1)
-      const size_t nt = (E + 15) / 16;
-      std::vector<uint8_t> b8(nt * 64 * 16, 0);
-      for (size_t t = 0; t < nt; ++t)
-        for (int l = 0; l < 64; ++l) {
-          const size_t e = 16 * t + (l & 15);
-          if (e >= E) continue;
-          for (int jj = 0; jj < 16; ++jj) {
-            const size_t k = 16 * (l >> 4) + jj;
-            if (k < S) b8[(t * 64 + l) * 16 + jj] = (uint8_t)((d1[k * nwords + e / 64] >> (e % 64)) & 1ull);
+      const size_t nt = (E + 15) / 16, kh = S > 64 ? 2 : 1;
+      std::vector<uint8_t> b8(kh * nt * 64 * 16, 0);
+      for (size_t h = 0; h < kh; ++h)
+        for (size_t t = 0; t < nt; ++t)
+          for (int l = 0; l < 64; ++l) {
+            const size_t e = 16 * t + (l & 15);
+            if (e >= E) continue;
+            for (int jj = 0; jj < 16; ++jj) {
+              const size_t k = 64 * h + 16 * (l >> 4) + jj;
+              if (k < S)
+                b8[((h * nt + t) * 64 + l) * 16 + jj] = (uint8_t)((d1[k * nwords + e / 64] >> (e % 64)) & 1ull);
+            }
           }
-        }
       // a second copy scaled by 64 follows (the B operand of the high digit of
-      // each pair; score_i8l_kernel loads it instead of shifting per tile)
+      // each pair; the log2 kernels load it instead of shifting per tile)
       const size_t nb = b8.size();
       b8.resize(2 * nb);
       for (size_t k = 0; k < nb; ++k) b8[nb + k] = (uint8_t)(b8[k] << 6);
@@ -865,7 +869,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 17) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..17", value);
+    if (value < 0 || value > 18) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..18", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }
@@ -901,7 +905,8 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "fact_kernel") == 0) *value = c.fact_kernel;
   else if (strcmp(name, "i8o") == 0) *value = c.i8o_ok ? (c.i8o_diag ? 2 : 1) : 0;
   else if (strcmp(name, "i8o_nodiag") == 0) *value = c.i8o_nodiag ? 1 : 0;
-  else if (strcmp(name, "i8l") == 0) *value = c.i8l_ok ? 1 : 0;
+  else if (strcmp(name, "i8l") == 0) *value = c.i8l_ok && c.fspad <= 64 ? 1 : 0;
+  else if (strcmp(name, "i8w") == 0) *value = c.i8w_ok ? 1 : 0;
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;

@@ -540,18 +540,24 @@ int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
   const bool i8cap = c.fspad <= 64 && c.d_B8 && ll_only;
   const bool wincap = ll_only && c.win_ok && cap >= 1 && cap <= kWinMaxCap;
   auto bnd = [&](int kind) { return host::fixed_point_bound(kind, c.i8_cexp, c.fx_colsum, c.S, c.E, cap); };
+  // the log2 kernel for 64 < S <= 128 (score_i8w_kernel)
+  const bool i8wcap = c.fspad == 128 && c.i8w_ok && c.d_B8 && ll_only;
   int fk = c.fact_kernel;
   if (fk == 0) {
     // auto: the capped lookup-table kernel for capped calls; else the fastest
     // int8 kernel whose worst-case ll error (nemo_host.h) stays within
-    // err_budget -- log2 fixed point (10), natural units (8), max offset (4)
-    // -- else the fp64 MFMA kernels
+    // err_budget -- log2 fixed point (10; 18 for S > 64), natural units (8),
+    // max offset (4) -- else the fp64 MFMA kernels
     if (wincap) fk = 9;
+    else if (i8wcap && bnd(host::kFxLog2) <= c.err_budget) fk = 18;
     else if (!i8cap) fk = 1;
     else if (c.i8o_ok && c.i8l_ok && bnd(host::kFxLog2) <= c.err_budget) fk = 10;
     else if (c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 8;
     else if (!c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 4;
     else fk = 2;
+  } else if (fk == 18) {
+    if (!ll_only || c.fspad != 128) fk = 1;
+    else if (!i8wcap) return -1;
   } else if (fk == 9 || fk == 15) {
     if (!wincap) return -1;
   } else if (fk == 2 || fk == 3) {
@@ -562,7 +568,7 @@ int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
     else if (fk >= 10 && !(c.i8o_ok && c.i8l_ok)) return -1;
   }
   if (bound) {
-    const bool l2 = fk >= 10 && fk != 15, nat = fk >= 4 && fk <= 8;
+    const bool l2 = fk >= 10 && fk != 15, nat = fk >= 4 && fk <= 8;  // (18: log2, S > 64)
     *bound = l2 ? bnd(host::kFxLog2) : nat ? bnd(host::kFxNatural) : 0.0;
   }
   return fk;
@@ -582,17 +588,18 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // waves; 13: register-stationary; 14: 8 waves compiled for 6 waves per
   // SIMD; 10 walks two effect tiles per iteration, 16 is the same kernel with
   // one; 17: 10's walk in persistent blocks that prep the next evaluation
-  // during the walk)
+  // during the walk; 18 the log2 kernel for 64 < S <= 128)
   const int fk = resolve_fact_kernel(c, cap, ll_only, nullptr);
   if (fk < 0) return hipErrorInvalidValue;  // asked for a kernel the staged model does not support
   const bool is_auto = c.fact_kernel == 0;
   const bool win = fk == 9 || fk == 15;
-  const bool l2 = fk >= 10 && fk != 15;
+  const bool wide = fk == 18;
+  const bool l2 = fk >= 10 && fk != 15 && !wide;
   const bool i8o = fk == 7 || fk == 8 || l2;
   const bool i8 = fk >= 4 && fk <= 6;
   const bool pipe = fk == 2 || fk == 3;
   hipError_t err = hipSuccess;
-  if (!i8 && !i8o && !win) {  // the int8 and lookup-table kernels derive their inputs themselves
+  if (!i8 && !i8o && !win && !wide) {  // the int8 and lookup-table kernels derive their inputs themselves
     prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
@@ -608,6 +615,8 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   bool finalized = false;
   if (win) {
     err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized, fk == 15);
+  } else if (wide) {
+    err = launch_score_i8w(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized);
   } else if (i8o) {
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block; 10 (auto's l2
     // choice): 8 waves, two effect tiles per iteration; 11: 4 waves; 12: 16;

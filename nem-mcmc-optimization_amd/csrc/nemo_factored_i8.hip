@@ -1695,6 +1695,238 @@ hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// score_i8w_kernel (fact_kernel 18): score_i8l_kernel for 64 < S <= 128.
+//
+// The contraction runs over K = 128 parents as two K = 64 halves per row
+// block, accumulated into the same int32 accumulators (|acc| < 2^20 for 128
+// parents: T_0 = acc_0 2^12 + acc_1 wraps mod 2^32 only transiently, its
+// true value is in (0, 2^31) by stage_i8o's |x| <= 690, as at S <= 64).  The
+// digits, G in the C-inits, the exp assembly from the integer accumulators
+// and the offset log-sum-exp are score_i8l_kernel's (7 slices, 2^-38 / ln 2
+// per entry).  Per evaluation the LDS holds A[7][2][128][64 B] = 112 KB, so
+// one 16-wave block runs per CU (4 waves per SIMD).  The walk takes one
+// 16-effect tile per iteration; partials are per pair of tiles (32 effects),
+// so even E = 700 gives the 16 waves 22 partials to share, and ll bits do
+// not depend on the batch size (one block per evaluation, in-kernel sum).
+// ---------------------------------------------------------------------------
+constexpr int kWideKH = 2;    // K halves
+constexpr int kWideSetT = 2;  // tiles per partial
+
+// i8l_digits into the two-half layout: slice sl, half j >> 6
+__device__ __forceinline__ void i8w_digits(int8_t* A8, int i, int j, double d) {
+  constexpr int SPAD = 128, SL = SPAD * 64;  // bytes per (slice, half)
+  const double hd = rint(d * kL2Scale);
+  const int h = (int)hd;
+  const int l = (int)rint(fma(d, kL2Scale, -hd) * 262144.0);
+  const int off = (j >> 6) * SL + a_byte<4>(i, j & 63);
+  const int hb = h + 32 * (1 + 64 + 4096), lb = l + 32 * (1 + 64);
+  A8[(0 * kWideKH) * SL + off] = (int8_t)(hb >> 18);
+  A8[(1 * kWideKH) * SL + off] = (int8_t)(((hb >> 12) & 63) - 32);
+  A8[(2 * kWideKH) * SL + off] = (int8_t)(((hb >> 6) & 63) - 32);
+  A8[(3 * kWideKH) * SL + off] = (int8_t)((hb & 63) - 32);
+  A8[(4 * kWideKH) * SL + off] = (int8_t)(lb >> 12);
+  A8[(5 * kWideKH) * SL + off] = (int8_t)(((lb >> 6) & 63) - 32);
+  A8[(6 * kWideKH) * SL + off] = (int8_t)((lb & 63) - 32);
+}
+
+// the prep passes of i8o_prep_passes with up to 127 parents per pair of
+// children: each pass covers its (child, parent) slots in kWideKH rounds of
+// 64 lanes; a lane's G terms of the pass are summed over the rounds, then
+// over the wave
+template <int WAVES, int KB>
+__device__ __forceinline__ void i8w_prep_passes(EvalLds e, int k0, int w, int lane, int S, int cap,
+                                                const double* __restrict__ w01b,
+                                                const double* __restrict__ elo_s,
+                                                const double* __restrict__ ehi_s,
+                                                const double2* __restrict__ ltab) {
+  const bool packed = cap == 0 || cap >= S - 1;
+  const int npass = packed ? (S + 1) / 2 : S;
+  int8_t* A8 = (int8_t*)e.A;
+  double ga[KB], gb[KB];
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) {
+    ga[kk] = 0.0;
+    gb[kk] = 0.0;
+    const int q = w + (k0 + kk) * WAVES;
+#pragma unroll
+    for (int hr = 0; hr < kWideKH; ++hr) {
+      const int p = lane + 64 * hr;
+      int qr = 0, pp = 0;
+      bool act = false, side_a = true;
+      if (q < npass) {
+        if (packed) {
+          const int q2 = S - 1 - q;
+          if (p < q) { qr = q; pp = p; act = true; }
+          else { qr = q2; pp = p - q; act = q2 != q && pp < q2; side_a = false; }
+        } else {
+          const int np = q < cap ? q : cap;
+          qr = q; pp = q - 1 - p; act = p < np;
+        }
+      }
+      if (act) {
+        const int i = e.perm[qr], j = e.perm[pp];
+        const double sw = w01b[i * S + j];
+        const double lo = log_fast(fma(sw, elo_s[j] - 1.0, 1.0), ltab);
+        const double d = log_fast(fma(sw, ehi_s[j] - 1.0, 1.0), ltab) - lo;
+        i8w_digits(A8, i, j, d);
+        if (side_a) ga[kk] += lo;
+        else gb[kk] += lo;
+      }
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < KB; ++kk) {
+    ga[kk] = wsum_dpp(ga[kk]);
+    gb[kk] = wsum_dpp(gb[kk]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int kk = 0; kk < KB; ++kk) {
+      const int q = w + (k0 + kk) * WAVES;
+      if (q >= npass) continue;
+      if (packed && S - 1 - q != q) e.G[e.perm[S - 1 - q]] = gb[kk];
+      e.G[e.perm[q]] = ga[kk];
+    }
+  }
+}
+
+template <int WAVES, int OCC>
+__global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8w_kernel(
+    int S, int E, int ntiles, int nsets, int cap, double padg,
+    const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi,
+    const uint8_t* __restrict__ B8, const int8_t* __restrict__ udig, const double* __restrict__ u0,
+    const double* __restrict__ nullsum, const void* __restrict__ tabs,
+    double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
+  constexpr int NR = 8, SPAD = NR * 16;
+  constexpr int NSL = 7;
+  extern __shared__ __attribute__((aligned(16))) double lds8[];
+  uint2* etab_o = (uint2*)lds8;                          // [kExpTabN] at LDS address 0
+  double2* ltab = (double2*)(etab_o + kExpTabN);         // [128] log table
+  double* elo_s = (double*)(ltab + 128);                 // [SPAD] e^lo_j
+  double* ehi_s = elo_s + SPAD;                          // [SPAD] e^hi_j
+  EvalLds ev;
+  ev.G = ehi_s + SPAD;                                   // [SPAD]
+  int* gi = (int*)(ev.G + SPAD);                         // [2][SPAD] g0, g1
+  ev.perm = gi + 2 * SPAD;                               // [SPAD]
+  ev.A = (i32x4*)(ev.perm + SPAD);                       // [NSL][KH][SPAD][4] swizzled (a_byte)
+
+  const int b = xcd_index8((int)blockIdx.x, (int)gridDim.x, remap);
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int col = lane & 15, rg = lane >> 4;
+
+  {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    const int4* src = (const int4*)tabs;
+    int4* dst = (int4*)lds8;
+    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
+    for (int i = tid; i < SPAD; i += blockDim.x) {
+      elo_s[i] = i < S ? e_lo[i] : 1.0;
+      ehi_s[i] = i < S ? e_hi[i] : 1.0;
+    }
+  }
+  i8_init_eval<SPAD, NSL * kWideKH, 4>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
+  __syncthreads();
+  {  // U' / ln 2 as the free diagonal "parent" i of child i
+    int8_t* A8 = (int8_t*)ev.A;
+    for (int k = tid; k < S * NSL; k += blockDim.x) {
+      const int i = k / NSL, sl = k - i * NSL;
+      A8[(sl * kWideKH + (i >> 6)) * SPAD * 64 + a_byte<4>(i, i & 63)] = udig[i * 8 + sl];
+    }
+  }
+  {
+    constexpr int KB = 2;
+    const int npass = i8_npass(S, cap);
+    const int my = npass > w ? (npass - w + WAVES - 1) / WAVES : 0;
+    for (int k0 = 0; k0 < my; k0 += KB)
+      i8w_prep_passes<WAVES, KB>(ev, k0, w, lane, S, cap, w01 + (size_t)b * S * S, elo_s, ehi_s, ltab);
+  }
+  __syncthreads();
+  // G + u0 in units of 2^-20 / ln 2 (score_i8l_kernel)
+  for (int i = tid; i < SPAD; i += blockDim.x) {
+    const double g = i < S ? ev.G[i] + u0[i] : ev.G[i];
+    const double g0 = rint(g * kL2Scale);
+    gi[i] = (int)g0 + (1023 << 20);
+    gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 262144.0);
+  }
+  __syncthreads();
+
+  const i32x4* Gi = (const i32x4*)gi;
+  const uint32_t a_lane = (uint32_t)(col * 4 + ((rg + 2 * (col >> 2)) & 3));  // swizzled chunk
+  // B fragments [x64][half][tile][lane] through a buffer resource
+  const __amdgpu_buffer_rsrc_t brs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)B8, (short)0, 2 * kWideKH * ntiles * kWave * 16, 0x00020000);
+  const uint32_t bln = (uint32_t)lane * 16u;
+  auto bload = [&](int tile, int x64, int h) {
+    return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         brs, bln, ((x64 * kWideKH + h) * ntiles + tile) * kWave * 16, 0));
+  };
+  for (int set = w; set < nsets; set += WAVES) {
+    double lprod = 1.0;
+    int lexp = 0;
+    const int t_end = min(ntiles, kWideSetT * set + kWideSetT);
+    for (int t = kWideSetT * set; t < t_end; ++t) {
+      const i32x4 b1[2] = {bload(t, 0, 0), bload(t, 0, 1)};
+      const i32x4 b64[2] = {bload(t, 1, 0), bload(t, 1, 1)};
+      uint32_t ao = a_lane;
+      asm volatile("" : "+v"(ao));
+      const i32x4* Al = ev.A + ao;
+      double ls0 = 0.0, ls1 = 0.0;
+#pragma unroll 2
+      for (int r = 0; r < NR; ++r) {
+        const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+        const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+        auto A = [&](int sl, int h) { return Al[((sl * kWideKH + h) * SPAD + 16 * r) * 4]; };
+        i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 0), b64[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
+        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 1), b64[1], h0, 0, 0, 0);
+        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 0), b1[0], h0, 0, 0, 0);
+        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 1), b1[1], h0, 0, 0, 0);
+        i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 0), b64[0], c0, 0, 0, 0);
+        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 1), b64[1], h1, 0, 0, 0);
+        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 0), b1[0], h1, 0, 0, 0);
+        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 1), b1[1], h1, 0, 0, 0);
+        i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 0), b1[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
+        l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 1), b1[1], l0, 0, 0, 0);
+        i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 0), b64[0], c1, 0, 0, 0);
+        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 1), b64[1], l1, 0, 0, 0);
+        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 0), b1[0], l1, 0, 0, 0);
+        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 1), b1[1], l1, 0, 0, 0);
+        uint32_t t0[4];
+        uint64_t evv[4];
+        double pr[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+          evv[g] = exp2_fx_load(t0[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+          else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+        }
+      }
+      const double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
+      lprod *= t * 16 + col < E ? l : 1.0;
+      lexp += __builtin_amdgcn_frexp_exp(lprod);
+      lprod = __builtin_amdgcn_frexp_mant(lprod);
+    }
+    // every 16-lane row holds the 16 column products (rowsum4)
+    double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
+    v = rowsum16(v);
+    if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const double v = sum_partials(partial + (size_t)b * nsets, nsets, lane);
+    if (lane == 0) ll_out[b] = v;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
@@ -1726,6 +1958,25 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
   }
 }
 
+hipError_t launch_score_i8w(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+  if (!c.i8w_ok || c.fspad != 128 || !c.d_nullsum_w || !c.d_B8 || !c.d_udig2 || !c.d_i8o_tabs)
+    return hipErrorInvalidValue;
+  constexpr int SPAD = 128, WAVES = 16, NSL = 7;
+  const int ntiles = (c.E + 15) / 16;
+  const int nsets = (ntiles + kWideSetT - 1) / kWideSetT;
+  const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)NSL * kWideKH * SPAD * 64;
+  hipError_t ae = hipFuncSetAttribute((const void*)score_i8w_kernel<WAVES, 4>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (ae != hipSuccess) return ae;
+  score_i8w_kernel<WAVES, 4><<<dim3(batch), WAVES * kWave, lds, st>>>(
+      c.S, c.E, ntiles, nsets, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8, c.d_udig2, c.d_u0,
+      c.d_nullsum_w, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+  *nparts = nsets;
+  *finalized = true;
+  return hipGetLastError();
+}
+
 // staging for score_i8o_kernel (after d_U64, e^lo / e^hi and the int8 scale):
 // U' = U - U[S] ((fspad + 1) rows, zero past S), sum_e U[S][e] per 8-tile set
 // (left fold), and the range checks that make the offset exp safe.
@@ -1734,15 +1985,18 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
   c.i8o_ok = false;
   c.i8o_diag = false;
   c.i8l_ok = false;
+  c.i8w_ok = false;
   for (void** p : {(void**)&c.d_Uoff, (void**)&c.d_nullsum, (void**)&c.d_udig, (void**)&c.d_u0,
-                   (void**)&c.d_udig2})
+                   (void**)&c.d_udig2, (void**)&c.d_nullsum_w})
     if (*p) {
       hipError_t fe = hipFree(*p);
       *p = nullptr;
       if (fe != hipSuccess) return fe;
     }
   const int S = c.S, E = c.E, SPAD = c.fspad;
-  if (!c.d_B8 || SPAD > 64 || SPAD < S) return hipSuccess;
+  // S <= 64: the int8 offset kernels; 64 < S <= 128: score_i8w_kernel (the
+  // same checks, the log2 form only)
+  if (!c.d_B8 || SPAD > 128 || SPAD < S) return hipSuccess;
   hipError_t err = hipStreamSynchronize(c.stream);
   if (err != hipSuccess) return err;
   std::vector<double> U((size_t)(S + 1) * E);
@@ -1889,6 +2143,21 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
         c.i8l_ok = true;
       }
     }
+  }
+  if (SPAD == 128 && c.i8l_ok) {
+    // score_i8w_kernel's partials cover 2 tiles (32 effects): sum_e U[S][e]
+    // per 32 effects, left fold
+    const int nsw = (ntiles + kWideSetT - 1) / kWideSetT;
+    std::vector<double> nw(nsw, 0.0);
+    for (int s2 = 0; s2 < nsw; ++s2) {
+      double acc = 0.0;
+      for (int e = 32 * s2; e < std::min(E, 32 * s2 + 32); ++e) acc += un[e];
+      nw[s2] = acc;
+    }
+    if ((err = hipMalloc((void**)&c.d_nullsum_w, nw.size() * 8)) != hipSuccess) return err;
+    if ((err = hipMemcpy(c.d_nullsum_w, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
+      return err;
+    c.i8w_ok = true;
   }
   if ((err = hipMalloc((void**)&c.d_Uoff, uo.size() * 8)) != hipSuccess) return err;
   if ((err = hipMalloc((void**)&c.d_nullsum, ns.size() * 8)) != hipSuccess) return err;

@@ -76,7 +76,8 @@ struct Ctx {
   double* d_fpartial = nullptr;    // [cap][factored_partials]
   // int8 matrix-core variant (S <= 64): fixed-point Delta digits
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
-  uint8_t* d_B8 = nullptr;         // [2][ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order,
+  uint8_t* d_B8 = nullptr;         // [2][KH][ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
+                                   // (KH = 1 K half for S <= 64, 2 for S <= 128),
                                    // then the same x 64
   // offset log-sum-exp variant (score_i8o_kernel), staged by stage_i8o
   bool i8o_ok = false;             // staging bounds hold: |cell - U[S]| <= 690
@@ -93,6 +94,9 @@ struct Ctx {
   bool i8l_ok = false;             // diagonal form and the fixed-point ranges hold
   int8_t* d_udig2 = nullptr;       // [S][8] digits of du_i / ln 2
   double* d_u0 = nullptr;          // [S] u0_i, added to G
+  // the same for 64 < S <= 128 (score_i8w_kernel; d_B8 then holds two K halves)
+  bool i8w_ok = false;
+  double* d_nullsum_w = nullptr;   // [ceil(ntiles / 2)] sum of U[S][e] per 32 effects
   // capped lookup-table variant (score_window_kernel), staged by stage_window
   bool win_ok = false;             // U - U[S] two-valued per row, partial sums in range
   double* d_wuw = nullptr;         // [S][2] U - U[S] of row i at D1 bit 0 / 1
@@ -180,6 +184,10 @@ hipError_t launch_score_i8(Ctx& c, int batch, int cap, const int32_t* d_pos, con
 hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                             double* d_ll, int waves, bool l2, hipStream_t st, int* nparts,
                             bool* finalized);
+// the log2 kernel for 64 < S <= 128 (c.i8w_ok): one block per evaluation,
+// ll written in-kernel (*finalized)
+hipError_t launch_score_i8w(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, hipStream_t st, int* nparts, bool* finalized);
 hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
                      const std::vector<uint64_t>& d1);
 // capped lookup-table kernel (nemo_window.hip): ll only, 1 <= cap <= kWinMaxCap,

@@ -27,6 +27,9 @@ CONFIGS = {
     "C2": (16, 500, 0, 0, "f64"),
     "C3": (64, 2000, 0, 0, "f64"),
     "C5": (128, 5000, 0, 6, "f32"),
+    # uncapped 64 < S <= 128 (the int8 log2 kernel for wide models,
+    # score_i8w_kernel; not a BASELINE config)
+    "W128": (128, 2000, 0, 0, "f64"),
 }
 
 

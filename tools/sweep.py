@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--batches", default="32,128,512")
     ap.add_argument("--fks", default="1,2,4,6,7,8")
     ap.add_argument("--out", default=os.path.join(HERE, "gpurun_out", "sweep.json"))
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused-step timings")
+    ap.add_argument("--no-stream", action="store_true", help="skip the streaming-kernel variants")
     args = ap.parse_args()
     import torch
     from scipy.special import expit
@@ -41,7 +43,7 @@ def main():
         # (batch, group, xcd_remap, path): path 1 = stream, 2 + 10 * fact_kernel = factored
         variants = []
         for batch in [int(v) for v in args.batches.split(",")]:
-            for group in ((1, 8) if cap == 0 else (1,)):
+            for group in (() if args.no_stream else ((1, 8) if cap == 0 else (1,))):
                 variants.append((batch, group, 1, 1))
             for fk in [int(v) for v in args.fks.split(",")]:  # 1 chunked, 2 f64 pipelined, 4/6 int8 x4/x8 waves, 7/8 offset int8 x4/x8
                 variants.append((batch, 1, 1, 2 + 10 * fk))
@@ -87,7 +89,7 @@ def main():
         eng.set_option("xcd_remap", 1)
         # fused per-step scorer (eval #1 + local optima + eval #2)
         from nemo.nem_order_mcmc import SIG0, SIG1
-        for nch in (1, 16):
+        for nch in (() if args.no_fused else (1, 16)):
             pos_h = np.array([rng.permutation(S) for _ in range(nch)], dtype=np.int32)
             w_h = rng.uniform(-3, 3, (nch, S, S))
             anc = np.clip(rng.random((nch, S, S)) - 0.5, 0, 1)
