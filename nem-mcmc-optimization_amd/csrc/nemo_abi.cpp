@@ -147,6 +147,8 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
     if (p) (void)hipFree(p);
   if (c.h_stage) (void)hipHostFree(c.h_stage);
   for (hipEvent_t ev : c.ev_pool) (void)hipEventDestroy(ev);
+  for (auto& g : c.step_graph)
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
   (void)hipStreamDestroy(c.stream);
   delete ctx;
 }
@@ -159,6 +161,7 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
   const size_t S = c.S, E = c.E;
   const int nb = std::max({max_batch, max_chains, 1});
   if (nb > c.cap_batch) {
+    ++c.graph_epoch;
     HIPCHK(hipStreamSynchronize(c.stream));
     HIPCHK(dalloc(&c.d_pos, nb * S));
     HIPCHK(dalloc(&c.d_w01, nb * S * S));
@@ -178,6 +181,7 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
   }
   const int nc = std::max(max_chains, 1);
   if (nc > c.cap_chains) {
+    ++c.graph_epoch;
     HIPCHK(hipStreamSynchronize(c.stream));
     HIPCHK(dalloc(&c.d_anc, nc * S * S));
     HIPCHK(dalloc(&c.d_pairs, nc * S * S));
@@ -197,6 +201,7 @@ namespace {
 // grow the pinned host staging buffer to at least `bytes`
 int host_stage(Ctx& c, size_t bytes) {
   if (bytes <= c.h_stage_bytes) return NEMO_OK;
+  ++c.graph_epoch;
   HIPCHK(hipStreamSynchronize(c.stream));
   if (c.h_stage) {
     HIPCHK(hipHostFree(c.h_stage));
@@ -211,6 +216,7 @@ int host_stage(Ctx& c, size_t bytes) {
 // grow the device block that mirrors the staging layout to at least `bytes`
 int dev_stage(Ctx& c, size_t bytes) {
   if (bytes <= c.d_step_bytes) return NEMO_OK;
+  ++c.graph_epoch;
   HIPCHK(hipStreamSynchronize(c.stream));
   if (c.d_step) {
     HIPCHK(hipFree(c.d_step));
@@ -228,6 +234,7 @@ int dev_stage(Ctx& c, size_t bytes) {
 // (the factored kernels read whole tiles; lanes past E are masked out)
 int alloc_tables(Ctx& c) {
   const size_t S = c.S, E = c.E;
+  ++c.graph_epoch;
   const size_t esz = c.dtype == NEMO_F64 ? 8 : 4;
   HIPCHK(hipStreamSynchronize(c.stream));
   c.staged = false;
@@ -252,6 +259,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
   Ctx& c = ctx->c;
   const size_t S = c.S, E = c.E;
   const int nwords = (int)((E + 63) / 64);
+  ++c.graph_epoch;
   c.factored = fact;
   c.i8o_ok = false;
   c.win_ok = false;
@@ -654,12 +662,61 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
   memcpy(hs + o_anc, anc, n * S * S * 8);
   memcpy(hs + o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
   memset(hs + o_inf, 0xff, n * S * S * 4);
-  HIPCHK(hipMemcpyAsync(ds, hs, o_ll1, hipMemcpyHostToDevice, st));
-  rc = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + o_w01),
-                                (const double*)(ds + o_anc), sig0, sig1, cap, (double*)(ds + o_wn),
-                                (double*)(ds + o_ll1), (double*)(ds + o_lld), (int32_t*)(ds + o_inf), st);
-  if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(hs + o_wn, ds + o_wn, total - o_wn, hipMemcpyDeviceToHost, st));
+  // the device work: one H2D copy of [pos .. info], the launches, one D2H copy
+  // of [w_new .. ll_dag]; replayed as a hipGraph per (nchains, cap) while no
+  // captured argument changes (the staging buffers, options and tables bump
+  // graph_epoch), so a step costs one graph launch instead of ~10 API calls
+  auto enqueue = [&]() -> int {
+    HIPCHK(hipMemcpyAsync(ds, hs, o_ll1, hipMemcpyHostToDevice, st));
+    int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + o_w01),
+                                     (const double*)(ds + o_anc), sig0, sig1, cap, (double*)(ds + o_wn),
+                                     (double*)(ds + o_ll1), (double*)(ds + o_lld), (int32_t*)(ds + o_inf), st);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(hs + o_wn, ds + o_wn, total - o_wn, hipMemcpyDeviceToHost, st));
+    return NEMO_OK;
+  };
+  Ctx::StepGraph* sg = nullptr;
+  if (c.graphs && !c.timing) {
+    for (auto& g : c.step_graph)
+      if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.sig0 == sig0 &&
+          g.sig1 == sig1)
+        sg = &g;
+    if (!sg) {  // capture once
+      Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
+      c.step_graph_next = (c.step_graph_next + 1) % 4;
+      if (g.exec) {
+        (void)hipGraphExecDestroy(g.exec);
+        g.exec = nullptr;
+      }
+      hipGraph_t graph = nullptr;
+      if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+        const int r = enqueue();
+        const hipError_t ee = hipStreamEndCapture(st, &graph);
+        if (r == NEMO_OK && ee == hipSuccess && graph &&
+            hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0) == hipSuccess) {
+          g.nchains = nchains;
+          g.cap = cap;
+          g.sig0 = sig0;
+          g.sig1 = sig1;
+          g.epoch = c.graph_epoch;
+          sg = &g;
+        } else {
+          g.exec = nullptr;
+          c.graphs = 0;  // this runtime does not capture the step: launch it directly from now on
+        }
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+      } else {
+        c.graphs = 0;
+      }
+    }
+  }
+  if (sg) {
+    HIPCHK(hipGraphLaunch(sg->exec, st));
+    c.ow_chains = nchains;  // nemo_optimal_weights_dev's host-side effect
+  } else if ((rc = enqueue())) {
+    return rc;
+  }
   HIPCHK(hipStreamSynchronize(st));
   memcpy(w_new, hs + o_wn, n * S * S * 8);
   memcpy(ll1, hs + o_ll1, n * 8);
@@ -864,6 +921,11 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!name) return fail(NEMO_ERR_ARG, "null option name");
+  ++ctx->c.graph_epoch;  // any option may change what a captured step launches
+  if (strcmp(name, "graphs") == 0) {
+    ctx->c.graphs = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "xcd_remap") == 0) {
     ctx->c.xcd_remap = value ? 1 : 0;
     return NEMO_OK;
@@ -908,6 +970,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "i8l") == 0) *value = c.i8l_ok && c.fspad <= 64 ? 1 : 0;
   else if (strcmp(name, "i8w") == 0) *value = c.i8w_ok ? 1 : 0;
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
+  else if (strcmp(name, "graphs") == 0) *value = c.graphs;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
@@ -920,6 +983,7 @@ int nemo_set_option_f64(nemo_ctx* ctx, const char* name, double value) {
   if (!name) return fail(NEMO_ERR_ARG, "null option name");
   if (strcmp(name, "err_budget") == 0) {
     if (!(value >= 0.0)) return fail(NEMO_ERR_ARG, "err_budget=%g must be >= 0", value);
+    ++ctx->c.graph_epoch;
     ctx->c.err_budget = value;
     return NEMO_OK;
   }
@@ -972,6 +1036,7 @@ int nemo_timing_enable(nemo_ctx* ctx, int enable) {
   if (rc) return rc;
   Ctx& c = ctx->c;
   HIPCHK(hipStreamSynchronize(c.stream));
+  ++c.graph_epoch;
   c.timing = enable != 0;
   c.ev_used = 0;
   c.launches = 0;

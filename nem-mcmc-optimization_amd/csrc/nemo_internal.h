@@ -128,6 +128,20 @@ struct Ctx {
   void* d_step = nullptr;
   size_t d_step_bytes = 0;
 
+  // hipGraphs of nemo_optimal_weights' device work (one H2D copy, the
+  // launches, one D2H copy) per (nchains, cap, sig0, sig1); graph_epoch moves
+  // whenever a captured argument may change (buffers, options, staging)
+  struct StepGraph {
+    int nchains = -1, cap = -1;
+    double sig0 = 0.0, sig1 = 0.0;
+    uint64_t epoch = 0;
+    hipGraphExec_t exec = nullptr;
+  };
+  int graphs = 1;                  // option "graphs": replay the fused step as a hipGraph
+  uint64_t graph_epoch = 1;
+  StepGraph step_graph[4];
+  int step_graph_next = 0;
+
   // timing of the score kernel
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;

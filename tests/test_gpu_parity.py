@@ -699,3 +699,45 @@ def test_split_local_optima_same_bits(n):
         for x, y in zip(out[mode], out[1]):
             assert np.array_equal(x, y), mode
     eng.set_option("local_split", 0)
+
+
+def test_fused_step_graph_replay_equals_direct_launches():
+    """nemo_optimal_weights replays its device work as a hipGraph per
+    (nchains, cap) (option "graphs", default 1): the same outputs as direct
+    launches, for several chain counts, a cap, and after an option change
+    (which must not replay a stale graph)."""
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(77)
+    cases = []
+    for n, cap in ((1, 0), (3, 0), (2, 5), (1, 0)):
+        pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
+        w = rng.uniform(-3, 3, (n, 64, 64))
+        anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
+        cases.append((pos, w, anc, cap))
+    def run_all():
+        return [eng.optimal_weights(p, expit(w), a, w, SIG0, SIG1, cap=cap, raise_on_fail=False)
+                for p, w, a, cap in cases]
+    eng.set_option("graphs", 1)
+    g1 = run_all()
+    g2 = run_all()            # replays
+    assert eng.get_option("graphs") == 1, "the fused step could not be captured"
+    eng.set_option("graphs", 0)
+    d = run_all()
+    for a, b, c in zip(g1, g2, d):
+        for x, y, z in zip(a, b, c):
+            assert np.array_equal(x, z) and np.array_equal(y, z)
+    # an option change between replays takes effect (fp64 eval #2 instead of int8)
+    eng.set_option("graphs", 1)
+    run_all()
+    eng.set_option("fact_kernel", 1)
+    f1 = run_all()
+    eng.set_option("graphs", 0)
+    f0 = run_all()
+    eng.set_option("fact_kernel", 0)
+    for a, c in zip(f1, f0):
+        for x, z in zip(a, c):
+            assert np.array_equal(x, z)
+    assert any(not np.array_equal(a[2], b[2]) for a, b in zip(f0, d))  # ll_dag moved: other kernel
+    eng.set_option("graphs", 1)
