@@ -204,7 +204,11 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                16 give one another's bits, within 1e-11 of 10's);
  *                15 = the round-1 form of 9 (row bits re-read from LDS);
  *                17 = 10's walk in persistent blocks that prep the next
- *                evaluation's digits during the walk (10's bits)
+ *                evaluation's digits during the walk (10's bits);
+ *                18 = the log2 kernel for 64 < S <= 128 (two K = 64 halves,
+ *                two tiles per iteration), which auto takes for uncapped
+ *                ll-only calls there within the error budget; 19 = the same
+ *                with one tile per iteration
  *   "factored"   (get only) 1 if the staged table is factorable
  *   "win"        (get only) 1 if the capped lookup-table kernel is staged
  *                (U - U[S] two-valued per row, partial sums in range)
@@ -214,6 +218,9 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *   "i8o_nodiag" 1 = keep the U reads even when 2 is available (testing)
  *   "i8l"        (get only) 1 if the log2 fixed-point offset kernel is staged
  *                (i8o = 2 and |Delta|, |U - U[S]| / ln 2 within its digit range)
+ *   "i8w"        (get only) 1 if the same is staged for 64 < S <= 128 (18 / 19)
+ *   "graphs"     1 (default): nemo_optimal_weights replays its device work
+ *                as a hipGraph per (nchains, cap); 0 = direct launches
  *   "local_split" 2 = run each local optimum of a fused step on a 4-wave
  *                block (the objective's products split over the waves; same
  *                bits; measured slower for one chain, so 0 = auto never

@@ -931,7 +931,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 18) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..18", value);
+    if (value < 0 || value > 19) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..19", value);
     ctx->c.fact_kernel = value;
     return NEMO_OK;
   }

@@ -555,7 +555,7 @@ int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
     else if (c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 8;
     else if (!c.i8o_ok && bnd(host::kFxNatural) <= c.err_budget) fk = 4;
     else fk = 2;
-  } else if (fk == 18) {
+  } else if (fk == 18 || fk == 19) {
     if (!ll_only || c.fspad != 128) fk = 1;
     else if (!i8wcap) return -1;
   } else if (fk == 9 || fk == 15) {
@@ -588,12 +588,13 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // waves; 13: register-stationary; 14: 8 waves compiled for 6 waves per
   // SIMD; 10 walks two effect tiles per iteration, 16 is the same kernel with
   // one; 17: 10's walk in persistent blocks that prep the next evaluation
-  // during the walk; 18 the log2 kernel for 64 < S <= 128)
+  // during the walk; 18 / 19 the log2 kernel for 64 < S <= 128 with two / one
+  // tiles per iteration)
   const int fk = resolve_fact_kernel(c, cap, ll_only, nullptr);
   if (fk < 0) return hipErrorInvalidValue;  // asked for a kernel the staged model does not support
   const bool is_auto = c.fact_kernel == 0;
   const bool win = fk == 9 || fk == 15;
-  const bool wide = fk == 18;
+  const bool wide = fk == 18 || fk == 19;
   const bool l2 = fk >= 10 && fk != 15 && !wide;
   const bool i8o = fk == 7 || fk == 8 || l2;
   const bool i8 = fk >= 4 && fk <= 6;
@@ -616,7 +617,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   if (win) {
     err = launch_score_window(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized, fk == 15);
   } else if (wide) {
-    err = launch_score_i8w(c, batch, cap, d_pos, d_w01, d_ll, st, &np, &finalized);
+    err = launch_score_i8w(c, batch, cap, d_pos, d_w01, d_ll, fk == 18, st, &np, &finalized);
   } else if (i8o) {
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block; 10 (auto's l2
     // choice): 8 waves, two effect tiles per iteration; 11: 4 waves; 12: 16;

@@ -1791,7 +1791,7 @@ __device__ __forceinline__ void i8w_prep_passes(EvalLds e, int k0, int w, int la
   }
 }
 
-template <int WAVES, int OCC>
+template <int WAVES, int OCC, bool TWO>
 __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8w_kernel(
     int S, int E, int ntiles, int nsets, int cap, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
@@ -1863,62 +1863,157 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8w_kernel(
     return __builtin_bit_cast(i32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                          brs, bln, ((x64 * kWideKH + h) * ntiles + tile) * kWave * 16, 0));
   };
-  for (int set = w; set < nsets; set += WAVES) {
-    double lprod = 1.0;
-    int lexp = 0;
-    const int t_end = min(ntiles, kWideSetT * set + kWideSetT);
-    for (int t = kWideSetT * set; t < t_end; ++t) {
-      const i32x4 b1[2] = {bload(t, 0, 0), bload(t, 0, 1)};
-      const i32x4 b64[2] = {bload(t, 1, 0), bload(t, 1, 1)};
+  if constexpr (TWO) {
+    // the set's two tiles a, b in one iteration: each A fragment is read once
+    // for both (half the LDS A traffic); rowsum_pair leaves tile a's column
+    // sums in rows 0 / 2 and tile b's in rows 1 / 3 (as score_i8l_kernel's
+    // two-tile walk).  A set of one tile (odd ntiles) repeats it and does not
+    // multiply the copy in.
+    for (int set = w; set < nsets; set += WAVES) {
+      const int ta = kWideSetT * set;
+      const bool two = ta + 1 < ntiles;
+      const int tb = two ? ta + 1 : ta;
+      const i32x4 b1a[2] = {bload(ta, 0, 0), bload(ta, 0, 1)}, b64a[2] = {bload(ta, 1, 0), bload(ta, 1, 1)};
+      const i32x4 b1b[2] = {bload(tb, 0, 0), bload(tb, 0, 1)}, b64b[2] = {bload(tb, 1, 0), bload(tb, 1, 1)};
       uint32_t ao = a_lane;
       asm volatile("" : "+v"(ao));
       const i32x4* Al = ev.A + ao;
-      double ls0 = 0.0, ls1 = 0.0;
-#pragma unroll 2
+      double la0 = 0.0, la1 = 0.0, lb0 = 0.0, lb1 = 0.0;
+#pragma unroll 1
       for (int r = 0; r < NR; ++r) {
         const i32x4 c0 = Gi[(16 * r) / 4 + rg];
         const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
         auto A = [&](int sl, int h) { return Al[((sl * kWideKH + h) * SPAD + 16 * r) * 4]; };
-        i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 0), b64[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
-        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 1), b64[1], h0, 0, 0, 0);
-        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 0), b1[0], h0, 0, 0, 0);
-        h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 1), b1[1], h0, 0, 0, 0);
-        i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 0), b64[0], c0, 0, 0, 0);
-        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 1), b64[1], h1, 0, 0, 0);
-        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 0), b1[0], h1, 0, 0, 0);
-        h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 1), b1[1], h1, 0, 0, 0);
-        i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 0), b1[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
-        l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 1), b1[1], l0, 0, 0, 0);
-        i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 0), b64[0], c1, 0, 0, 0);
-        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 1), b64[1], l1, 0, 0, 0);
-        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 0), b1[0], l1, 0, 0, 0);
-        l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 1), b1[1], l1, 0, 0, 0);
-        uint32_t t0[4];
-        uint64_t evv[4];
-        double pr[4];
+        i32x4 h0a = i32x4{0, 0, 0, 0}, h0b = i32x4{0, 0, 0, 0}, h1a = c0, h1b = c0;
+        i32x4 l0a = i32x4{0, 0, 0, 0}, l0b = i32x4{0, 0, 0, 0}, l1a = c1, l1b = c1;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
-          evv[g] = exp2_fx_load(t0[g]);
+        for (int h = 0; h < kWideKH; ++h) {
+          {
+            const i32x4 a = A(0, h);
+            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a[h], h0a, 0, 0, 0);
+            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b[h], h0b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(1, h);
+            h0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a[h], h0a, 0, 0, 0);
+            h0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b[h], h0b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(2, h);
+            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a[h], h1a, 0, 0, 0);
+            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b[h], h1b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(3, h);
+            h1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a[h], h1a, 0, 0, 0);
+            h1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b[h], h1b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(4, h);
+            l0a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a[h], l0a, 0, 0, 0);
+            l0b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b[h], l0b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(5, h);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64a[h], l1a, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b64b[h], l1b, 0, 0, 0);
+          }
+          {
+            const i32x4 a = A(6, h);
+            l1a = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1a[h], l1a, 0, 0, 0);
+            l1b = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b1b[h], l1b, 0, 0, 0);
+          }
         }
+        auto epi = [&](const i32x4 h0, const i32x4 h1, const i32x4 l0, const i32x4 l1, double& ls0,
+                       double& ls1) {
+          uint32_t t0[4];
+          uint64_t evv[4];
+          double pr[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+          for (int g = 0; g < 4; ++g) {
+            t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+            evv[g] = exp2_fx_load(t0[g]);
+          }
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
-          else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
-        }
+          for (int g = 0; g < 4; ++g)
+            pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+            else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+          }
+        };
+        epi(h0a, h1a, l0a, l1a, la0, la1);
+        epi(h0b, h1b, l0b, l1b, lb0, lb1);
       }
-      const double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
-      lprod *= t * 16 + col < E ? l : 1.0;
-      lexp += __builtin_amdgcn_frexp_exp(lprod);
-      lprod = __builtin_amdgcn_frexp_mant(lprod);
+      const double l = rowsum_pair(la0 + la1, lb0 + lb1) + 1.0;  // + e^0 of the null row
+      const bool tile_b = (lane & 16) != 0;
+      const bool ok = (((tile_b ? tb : ta) * 16 + col) < E) & (two | !tile_b);
+      const double lprod = ok ? l : 1.0;  // one factor per lane: no renormalisation
+      // rows 0 / 1 hold tile a's / tile b's 16 column values
+      double v = log_fast(lprod, ltab);
+      v = rowsum16(v);
+      v += __shfl_down(v, 16, kWave);
+      if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
     }
-    // every 16-lane row holds the 16 column products (rowsum4)
-    double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
-    v = rowsum16(v);
-    if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+  } else {
+    for (int set = w; set < nsets; set += WAVES) {
+      double lprod = 1.0;
+      int lexp = 0;
+      const int t_end = min(ntiles, kWideSetT * set + kWideSetT);
+      for (int t = kWideSetT * set; t < t_end; ++t) {
+        const i32x4 b1[2] = {bload(t, 0, 0), bload(t, 0, 1)};
+        const i32x4 b64[2] = {bload(t, 1, 0), bload(t, 1, 1)};
+        uint32_t ao = a_lane;
+        asm volatile("" : "+v"(ao));
+        const i32x4* Al = ev.A + ao;
+        double ls0 = 0.0, ls1 = 0.0;
+  #pragma unroll 2
+        for (int r = 0; r < NR; ++r) {
+          const i32x4 c0 = Gi[(16 * r) / 4 + rg];
+          const i32x4 c1 = Gi[(SPAD + 16 * r) / 4 + rg];
+          auto A = [&](int sl, int h) { return Al[((sl * kWideKH + h) * SPAD + 16 * r) * 4]; };
+          i32x4 h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 0), b64[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
+          h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(0, 1), b64[1], h0, 0, 0, 0);
+          h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 0), b1[0], h0, 0, 0, 0);
+          h0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(1, 1), b1[1], h0, 0, 0, 0);
+          i32x4 h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 0), b64[0], c0, 0, 0, 0);
+          h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(2, 1), b64[1], h1, 0, 0, 0);
+          h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 0), b1[0], h1, 0, 0, 0);
+          h1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(3, 1), b1[1], h1, 0, 0, 0);
+          i32x4 l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 0), b1[0], i32x4{0, 0, 0, 0}, 0, 0, 0);
+          l0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(4, 1), b1[1], l0, 0, 0, 0);
+          i32x4 l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 0), b64[0], c1, 0, 0, 0);
+          l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(5, 1), b64[1], l1, 0, 0, 0);
+          l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 0), b1[0], l1, 0, 0, 0);
+          l1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A(6, 1), b1[1], l1, 0, 0, 0);
+          uint32_t t0[4];
+          uint64_t evv[4];
+          double pr[4];
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            t0[g] = ((uint32_t)h0[g] << 12) + (uint32_t)h1[g];
+            evv[g] = exp2_fx_load(t0[g]);
+          }
+  #pragma unroll
+          for (int g = 0; g < 4; ++g)
+            pr[g] = exp2_fx_series(t0[g], (int)(((uint32_t)l0[g] << 12) + (uint32_t)l1[g]));
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if (g & 1) ls1 = exp2_fx_apply(t0[g], evv[g], pr[g], ls1);
+            else ls0 = exp2_fx_apply(t0[g], evv[g], pr[g], ls0);
+          }
+        }
+        const double l = rowsum4(ls0 + ls1) + 1.0;  // + e^0 of the null row
+        lprod *= t * 16 + col < E ? l : 1.0;
+        lexp += __builtin_amdgcn_frexp_exp(lprod);
+        lprod = __builtin_amdgcn_frexp_mant(lprod);
+      }
+      // every 16-lane row holds the 16 column products (rowsum4)
+      double v = log_fast(lprod, ltab) + (double)lexp * 0.69314718055994530942;
+      v = rowsum16(v);
+      if (lane == 0) partial[(size_t)b * nsets + set] = nullsum[set] + v;
+    }
   }
   __syncthreads();
   if (w == 0) {
@@ -1958,23 +2053,31 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
   }
 }
 
-hipError_t launch_score_i8w(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                            double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
+template <bool TWO>
+hipError_t launch_i8w_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                        double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   if (!c.i8w_ok || c.fspad != 128 || !c.d_nullsum_w || !c.d_B8 || !c.d_udig2 || !c.d_i8o_tabs)
     return hipErrorInvalidValue;
   constexpr int SPAD = 128, WAVES = 16, NSL = 7;
   const int ntiles = (c.E + 15) / 16;
   const int nsets = (ntiles + kWideSetT - 1) / kWideSetT;
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)NSL * kWideKH * SPAD * 64;
-  hipError_t ae = hipFuncSetAttribute((const void*)score_i8w_kernel<WAVES, 4>,
+  hipError_t ae = hipFuncSetAttribute((const void*)score_i8w_kernel<WAVES, 4, TWO>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (ae != hipSuccess) return ae;
-  score_i8w_kernel<WAVES, 4><<<dim3(batch), WAVES * kWave, lds, st>>>(
+  score_i8w_kernel<WAVES, 4, TWO><<<dim3(batch), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8, c.d_udig2, c.d_u0,
       c.d_nullsum_w, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = true;
   return hipGetLastError();
+}
+
+// fact_kernel 18: two tiles per iteration (auto); 19: one
+hipError_t launch_score_i8w(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            double* d_ll, bool two, hipStream_t st, int* nparts, bool* finalized) {
+  return two ? launch_i8w_t<true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)
+             : launch_i8w_t<false>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized);
 }
 
 // staging for score_i8o_kernel (after d_U64, e^lo / e^hi and the int8 scale):

@@ -201,7 +201,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
 // the log2 kernel for 64 < S <= 128 (c.i8w_ok): one block per evaluation,
 // ll written in-kernel (*finalized)
 hipError_t launch_score_i8w(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
-                            double* d_ll, hipStream_t st, int* nparts, bool* finalized);
+                            double* d_ll, bool two, hipStream_t st, int* nparts, bool* finalized);
 hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<double>& ehi,
                      const std::vector<uint64_t>& d1);
 // capped lookup-table kernel (nemo_window.hip): ll only, 1 <= cap <= kWinMaxCap,

@@ -42,6 +42,12 @@ def test_wide_kernel_vs_oracle(s, e):
     ll = eng.score(pos, w01)
     ref = np.array([no.order_score(m.U, t, perms[c], w01[c]) for c in range(n)])
     assert np.max(np.abs(ll - ref)) <= min(1e-6, bound + FP64_NOISE)
+    # 19: the same kernel walking one tile per iteration (its own bits)
+    eng.set_option("fact_kernel", 19)
+    assert eng.score_kernel(0) == (19, bound)
+    ll19 = eng.score(pos, w01)
+    assert np.max(np.abs(ll19 - ref)) <= min(1e-6, bound + FP64_NOISE)
+    assert eng.score(pos[1:2], w01[1:2])[0] == ll19[1]
     # the fp64 kernels on the same inputs (pipelined: ll only; chunked)
     for k in (1,):
         eng.set_option("fact_kernel", k)
