@@ -248,6 +248,8 @@ def c5_capped(torch, dist, stream, batch=2048, steps=10, warmup_s=0.3):
 
 
 KERNEL_NAMES = {
+    "i8w": "score_i8w_kernel (score_i8l_kernel's arithmetic for 64 < S <= 128: K = 128 as two K = 64 "
+           "halves per row block, two tiles per iteration)",
     "i8l": "score_i8l_kernel (x / ln 2 = Delta.D1 + U' + G exact in int8 fixed point on "
            "v_mfma_i32_16x16x64_i8, 7 digit slices; e^x assembled from the integer accumulators + "
            "table + degree-2 series; log-sum-exp offset by the null row; two 16-effect tiles per "
@@ -262,6 +264,7 @@ KERNEL_NAMES = {
 }
 ARITH = {
     "i8l": "int8 fixed point 2^-38/ln2 + fp64 LSE",
+    "i8w": "int8 fixed point 2^-38/ln2 + fp64 LSE",
     "i8o": "int8 fixed point 2^-44 + fp64 LSE",
     "i8": "int8 fixed point 2^-44 + fp64 LSE",
 }
@@ -269,6 +272,8 @@ ARITH = {
 
 def kernel_tag(fk):
     """profiles/*.json key tag of the kernel fact_kernel ``fk`` launches."""
+    if fk in (18, 19):
+        return "i8w"
     if fk in (10, 11, 12, 14, 16, 17):
         return "i8l"
     if fk == 13:
@@ -294,11 +299,13 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
     fpe = algorithmic_flops_per_eval(S, E, cap)
     f64eq = B * fpe / kern_s / 1e12
     secondary = {}
-    if tag in ("i8l", "i8o", "i8s"):
+    if tag in ("i8l", "i8o", "i8s", "i8w"):
         # the MFMAs the kernel issues: 7 (log2) or 8 v_mfma_i32_16x16x64_i8
         # (2*16*16*64 ops each) per 16-child row block per 16-effect tile
+        # (per K = 64 half: two halves for 64 < S <= 128)
         nslice = 7 if tag != "i8o" else 8
-        ops = ((E + 15) // 16) * (4 if S > 32 else 2 if S > 16 else 1) * nslice * 32768
+        nr = 8 if S > 64 else 4 if S > 32 else 2 if S > 16 else 1
+        ops = ((E + 15) // 16) * nr * nslice * (2 if S > 64 else 1) * 32768
         a = B * ops / kern_s / 1e12
         secondary["int8_mfma"] = {"achieved": a, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                                   "frac": a / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops}
@@ -335,13 +342,49 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
         roof.update({"bound": "mfma", "achieved": f64eq, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                      "frac": f64eq / F64_MFMA_PEAK_TF, "note": "fp64 MFMA contraction 2*P*E FLOP per evaluation"})
     roof["secondary"] = secondary
-    if tag in ("i8l", "i8o", "i8s", "i8"):
+    if tag in ("i8l", "i8o", "i8s", "i8", "i8w"):
         roof["fp64_equivalent"] = {
             "achieved": f64eq, "unit": "TFLOP/s", "flops_per_eval": fpe, "vs_f64_mfma_peak": f64eq / F64_MFMA_PEAK_TF,
             "note": "the contraction Delta.D1 priced as fp64 work (2*P*E FLOP/eval) against the fp64 MFMA peak: "
                     "how far the int8 fixed-point reformulation is past an fp64 matrix-core roofline; not a "
                     "hardware fraction"}
     return roof
+
+
+def wide_uncapped(torch, dist, stream, batch=2048, steps=5, warmup_s=0.3):
+    """Uncapped 64 < S <= 128 (generator config W128: 128 x 2000): the int8
+    log2 kernel for wide models (fact_kernel 18, what auto takes within the
+    error budget) next to the fp64 MFMA kernel it replaces (fact_kernel 1),
+    on the same resident inputs; kernel time per launch from HIP events."""
+    from scipy.special import expit
+
+    from nemo import generator
+    from nemo.engine import Engine
+    S, E, _seed, cap, dtype = generator.CONFIGS["W128"]
+    eng = Engine.for_nem(generator.config_nem("W128"), dtype=dtype)
+    eng.reserve(batch)
+    rng = np.random.default_rng(79)
+    d_pos = torch.from_numpy(np.array([rng.permutation(S) for _ in range(batch)], dtype=np.int32)).cuda()
+    d_w01 = torch.from_numpy(expit(rng.uniform(-3, 3, (batch, S, S)))).cuda()
+    d_ll = torch.zeros(batch, dtype=torch.float64, device="cuda")
+    fk_auto, bound = eng.score_kernel(0)
+    out = {"workload": f"W128: S={S} E={E} uncapped {dtype}, {batch} evaluations per launch",
+           "auto_fact_kernel": fk_auto, "ll_error_bound": bound}
+    lls = {}
+    for name, fk in (("int8_log2_wide_kernel", 18), ("f64_mfma_factored_kernel", 1)):
+        eng.set_option("fact_kernel", fk)
+        wall, kms, _ = timed_steps(eng, torch, batch, cap, steps, 1, d_pos, d_w01, d_ll, stream, 1, dist,
+                                   warmup_s=warmup_s)
+        lls[name] = d_ll.cpu().numpy()
+        out[name] = {"evals_per_s": batch * steps / wall, "kernel_avg_ms": kms,
+                     "cells_per_s": batch * S * E / (kms / 1e3)}
+    out["int8_log2_wide_kernel"]["kernel"] = ("score_i8w_kernel (score_i8l_kernel's arithmetic over K = 128 as "
+                                              "two K = 64 halves; two tiles per iteration)")
+    out["speedup_vs_f64"] = (out["f64_mfma_factored_kernel"]["kernel_avg_ms"] /
+                             out["int8_log2_wide_kernel"]["kernel_avg_ms"])
+    out["max_abs_ll_diff"] = float(np.max(np.abs(lls["int8_log2_wide_kernel"] - lls["f64_mfma_factored_kernel"])))
+    eng.close()
+    return out
 
 
 def main():
@@ -516,6 +559,8 @@ def main():
             # BASELINE config C5 (128 x 5000, parent cap 6): the capped
             # lookup-table kernel next to the fp64 MFMA factored kernel
             extras["c5_capped"] = c5_capped(torch, dist, stream, warmup_s=min(args.warmup_seconds, 0.3))
+            # uncapped 64 < S <= 128: the wide int8 kernel next to the fp64 one
+            extras["wide_uncapped"] = wide_uncapped(torch, dist, stream, warmup_s=min(args.warmup_seconds, 0.3))
 
     if rank == 0:
         if factored:

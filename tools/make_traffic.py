@@ -24,7 +24,7 @@ def per_kernel(path, counter):
             continue
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
         for tag, kind in (("score_window2_kernel", "win2"), ("score_window_kernel", "win"),
-                          ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"),
+                          ("score_i8w_kernel", "i8w"), ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"),
                           ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
                           ("score_factored_kernel", "factored"), ("score_kernel", "stream")):
             if tag in name:

@@ -18,7 +18,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
 from nemo.build import build_id  # noqa: E402  (the record names the build it measured)
 
-TAGS = (("score_window2_kernel", "win2"), ("score_window_kernel", "win"), ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
+TAGS = (("score_window2_kernel", "win2"), ("score_window_kernel", "win"), ("score_i8w_kernel", "i8w"), ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
         ("score_factored_kernel", "factored"), ("score_kernel", "stream"))
 
 
