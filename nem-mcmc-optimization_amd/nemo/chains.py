@@ -140,28 +140,33 @@ def opt_weights_batch(chains, engine: Engine, cap=0):
 
 
 def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0,
-                raise_on_fail=True, pool=None):
+                raise_on_fail=True, pool=None, state=None, return_state=False):
     """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
     lock-step: each MCMC step is one fused device call per chain group.  Chain k
     draws from ``chains[k].rng`` in the reference's call order, and ends with
     the attributes its own ``method`` call would leave (best_score, best_dag,
     best_order, score lists, parents_list of the best order).  Returns the
-    per-chain best scores.  If a local optimisation fails and
+    per-chain best scores (and, with ``return_state``, the loop state:
+    passed back as ``state`` it continues the same run as if it had not
+    stopped -- ``ChainBatch.run(n, resume=True)`` and its checkpoints).  If a local optimisation fails and
     ``raise_on_fail`` is set, the reference's Exception propagates and the
     chains' states are unspecified afterwards (see the pipeline below).
     ``pool`` (an ``InvPool``) runs the ancestor_x inversions in worker
     processes; the results do not change."""
     n = len(chains)
     s = chains[0].num_s
-    optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail, pool=pool)
-    curr = list(opt_weights_batch(chains, engine, cap=cap))
-    st = []
-    for k, c in enumerate(chains):
-        dag, _ = c.create_dag(c.parent_weights)
-        st.append(dict(best=curr[k], best_dag=dag, curr_perm=c.perm_order, best_order=c.perm_order,
-                       best_order_list=[c.perm_order], curr_dag=np.zeros((s, s)),
-                       curr_list=[curr[k]], best_list=[curr[k]], all_list=[curr[k]],
-                       best_parents=c.parents_list.copy(), best_struct=(c._pos, c._mask), acc=[]))
+    if state is None:
+        optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap, raise_on_fail=raise_on_fail, pool=pool)
+        curr = list(opt_weights_batch(chains, engine, cap=cap))
+        st = []
+        for k, c in enumerate(chains):
+            dag, _ = c.create_dag(c.parent_weights)
+            st.append(dict(best=curr[k], best_dag=dag, curr_perm=c.perm_order, best_order=c.perm_order,
+                           best_order_list=[c.perm_order], curr_dag=np.zeros((s, s)),
+                           curr_list=[curr[k]], best_list=[curr[k]], all_list=[curr[k]],
+                           best_parents=c.parents_list.copy(), best_struct=(c._pos, c._mask), acc=[]))
+    else:
+        st, curr = state["st"], state["curr"]
     props = [None] * n
 
     def propose(idx):
@@ -245,7 +250,8 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         c.accepted = q["acc"]
         c.parents_list = q["best_parents"]
         c._pos, c._mask = q["best_struct"]
-    return np.array([q["best"] for q in st])
+    best = np.array([q["best"] for q in st])
+    return (best, {"st": st, "curr": curr}) if return_state else best
 
 
 class ChainBatch:
@@ -278,6 +284,7 @@ class ChainBatch:
         if inv_pool is not None and (inv_pool.s != nem.num_s or inv_pool.maxb < len(init_orders)):
             raise ValueError("inv_pool: matrix size or capacity does not fit this batch")
         self.inv_pool = inv_pool
+        self._state = None
         self.chains = []
         for order, seed in zip(init_orders, seeds):
             c = NEMOrderMCMC(nem, np.asarray(order), engine=self.engine, cap=cap)
@@ -285,16 +292,93 @@ class ChainBatch:
             self.chains.append(c)
         self.engine.reserve(self.n, self.n)
 
-    def run(self, n_iterations: int):
+    def run(self, n_iterations: int, resume: bool = False):
         """Every chain runs the reference's ``method`` loop
         (nem_order_mcmc.py:257-310) for ``n_iterations`` steps.  Returns
-        (best scores [n], best orders [n, S])."""
-        self.best_scores = run_methods(self.chains, self.gammas, n_iterations, self.engine,
-                                       swap_prob=self.swap_prob, use_nem=self.use_nem, cap=self.cap,
-                                       raise_on_fail=self.raise_on_fail, pool=self.inv_pool)
+        (best scores [n], best orders [n, S]).  ``resume=True`` continues the
+        previous run (or the checkpoint this batch was restored from) for
+        ``n_iterations`` more steps, exactly as one longer run would;
+        ``accepted`` then covers the whole run."""
+        if resume and self._state is None:
+            raise ValueError("resume=True: no run or checkpoint to continue")
+        self.best_scores, self._state = run_methods(
+            self.chains, self.gammas, n_iterations, self.engine, swap_prob=self.swap_prob, use_nem=self.use_nem,
+            cap=self.cap, raise_on_fail=self.raise_on_fail, pool=self.inv_pool,
+            state=self._state if resume else None, return_state=True)
         self.best_orders = [np.asarray(c.best_order).copy() for c in self.chains]
-        self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(n_iterations, self.n)
+        self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(-1, self.n)
         return self.best_scores, np.stack(self.best_orders)
+
+    # -- checkpoint / resume of the chain states (SURVEY.md 5) ----------------
+    def save_checkpoint(self, path: str):
+        """Every chain's state after ``run`` -- weights, order, random stream,
+        and the loop state (current / best order and score, the score and
+        accept lists) -- to one ``.npz`` of plain arrays (no pickle).
+        ``ChainBatch.from_checkpoint`` + ``run(n, resume=True)`` continues
+        bit for bit as if the run had not stopped."""
+        import json
+        if self._state is None:
+            raise ValueError("save_checkpoint: run() first")
+        st, curr = self._state["st"], self._state["curr"]
+        arr = {}
+        meta = {"n": self.n, "num_s": self.nem.num_s, "num_e": self.nem.num_e, "gammas": self.gammas.tolist(),
+                "swap_prob": self.swap_prob, "use_nem": self.use_nem, "cap": self.cap,
+                "raise_on_fail": self.raise_on_fail, "curr": [float(v) for v in curr], "chains": []}
+        for k, (c, q) in enumerate(zip(self.chains, st)):
+            arr[f"c{k}.w"] = np.asarray(c.parent_weights, dtype=np.float64)
+            arr[f"c{k}.perm"] = np.asarray(c._perm)
+            version, mt, gauss = c.rng.getstate()
+            arr[f"c{k}.rng"] = np.asarray(mt, dtype=np.int64)
+            for a in ("best_dag", "curr_perm", "best_order", "curr_dag"):
+                arr[f"c{k}.{a}"] = np.asarray(q[a])
+            arr[f"c{k}.best_order_list"] = np.stack([np.asarray(o) for o in q["best_order_list"]])
+            arr[f"c{k}.best_pos"] = np.asarray(q["best_struct"][0])
+            for a in ("curr_list", "best_list", "all_list"):
+                arr[f"c{k}.{a}"] = np.asarray(q[a], dtype=np.float64)
+            arr[f"c{k}.acc"] = np.asarray(q["acc"], dtype=bool)
+            meta["chains"].append({"ll": float(c.ll), "best": float(q["best"]), "rng_version": version,
+                                   "rng_gauss": gauss})
+        arr["meta"] = np.asarray(json.dumps(meta))
+        np.savez_compressed(path, **arr)
+
+    @classmethod
+    def from_checkpoint(cls, path: str, nem, engine: Engine | None = None, inv_pool=None):
+        """A batch in the state ``save_checkpoint`` wrote; ``nem`` is the same
+        model (checked by shape).  Continue it with ``run(n, resume=True)``."""
+        import json
+        z = np.load(path, allow_pickle=False)
+        meta = json.loads(str(z["meta"]))
+        if (meta["num_s"], meta["num_e"]) != (nem.num_s, nem.num_e):
+            raise ValueError("checkpoint of another model shape")
+        n = meta["n"]
+        self = cls(nem, [z[f"c{k}.perm"] for k in range(n)], seeds=list(range(n)), engine=engine,
+                   gamma=np.asarray(meta["gammas"]), swap_prob=meta["swap_prob"], use_nem=meta["use_nem"],
+                   cap=meta["cap"], on_fail="raise" if meta["raise_on_fail"] else "continue", inv_pool=inv_pool)
+        st = []
+        for k, c in enumerate(self.chains):
+            cm = meta["chains"][k]
+            perm = np.array(z[f"c{k}.perm"])
+            # the structures reset() leaves for this order; W is the saved one
+            # (reset's quirks already applied to it)
+            c.get_permissible_parents(perm, init=True, init_value=1.0)
+            c.parent_weights = np.array(z[f"c{k}.w"], dtype=np.float64)
+            c.perm_order = perm
+            c.ll = cm["ll"]
+            c.rng.setstate((cm["rng_version"], tuple(int(v) for v in z[f"c{k}.rng"]), cm["rng_gauss"]))
+            bpos = np.array(z[f"c{k}.best_pos"])
+            bperm = np.argsort(bpos)
+            best_parents = np.empty(nem.num_s, dtype=object)
+            for i in range(nem.num_s):
+                best_parents[i] = c._parents_of(bperm, bpos, i)
+            st.append(dict(best=cm["best"], best_dag=np.array(z[f"c{k}.best_dag"]),
+                           curr_perm=np.array(z[f"c{k}.curr_perm"]), best_order=np.array(z[f"c{k}.best_order"]),
+                           best_order_list=list(np.array(z[f"c{k}.best_order_list"])),
+                           curr_dag=np.array(z[f"c{k}.curr_dag"]),
+                           curr_list=z[f"c{k}.curr_list"].tolist(), best_list=z[f"c{k}.best_list"].tolist(),
+                           all_list=z[f"c{k}.all_list"].tolist(), best_parents=best_parents,
+                           best_struct=(bpos, c._permissible(bpos)), acc=z[f"c{k}.acc"].tolist()))
+        self._state = {"st": st, "curr": list(meta["curr"])}
+        return self
 
 
 def gather_best(best_scores, best_orders, device=None):

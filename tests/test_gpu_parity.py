@@ -741,3 +741,32 @@ def test_fused_step_graph_replay_equals_direct_launches():
             assert np.array_equal(x, z)
     assert any(not np.array_equal(a[2], b[2]) for a, b in zip(f0, d))  # ll_dag moved: other kernel
     eng.set_option("graphs", 1)
+
+
+def test_chain_checkpoint_resume_equals_one_run(tmp_path):
+    """ChainBatch.save_checkpoint / from_checkpoint + run(n, resume=True):
+    3 + 4 steps with a checkpoint in between give exactly the 7-step run
+    (accepts, scores, best orders, every chain's random stream)."""
+    from nemo.chains import ChainBatch
+    m = generator.synthetic_nem(16, 500, 0)
+    orders = [np.random.default_rng(k).permutation(16) for k in range(4)]
+    seeds = [21, 22, 23, 24]
+    one = ChainBatch(m, orders, seeds, swap_prob=0.9)
+    b1, o1 = one.run(7)
+    part = ChainBatch(m, orders, seeds, swap_prob=0.9, engine=one.engine)
+    part.run(3)
+    path = str(tmp_path / "chains.npz")
+    part.save_checkpoint(path)
+    back = ChainBatch.from_checkpoint(path, m, engine=one.engine)
+    b2, o2 = back.run(4, resume=True)
+    assert np.array_equal(b1, b2) and np.array_equal(o1, o2)
+    assert np.array_equal(back.accepted, one.accepted)
+    for c1, c2 in zip(one.chains, back.chains):
+        assert c1.rng.getstate() == c2.rng.getstate()
+        assert np.array_equal(c1.parent_weights, c2.parent_weights)
+        assert c1.all_score_list == c2.all_score_list
+    # resuming the in-memory batch is the same as resuming the checkpoint
+    b3, _ = part.run(4, resume=True)
+    assert np.array_equal(b3, b1)
+    with pytest.raises(ValueError, match="resume"):
+        ChainBatch(m, orders, seeds, engine=one.engine).run(1, resume=True)
