@@ -320,8 +320,9 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
                             "bank_conflict_share": valu.get("SQ_LDS_BANK_CONFLICT", 0.0) / valu["SQ_LDS_IDX_ACTIVE"]}
     roof = {"kernel": KERNEL_NAMES.get(tag, tag), "fact_kernel": fk, "kernel_avg_ms": kern_ms,
             "kernel_avg_ms_launch_events": launch_ev_ms,
-            "traffic": traffic["bytes_per_launch"] / B if traffic else None,
-            "traffic_unit": "HBM bytes per evaluation (PMC, this build)" if traffic else None}
+            "traffic": traffic["bytes_per_launch"] if traffic else None,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, this build)" if traffic else None,
+            "evals_per_launch": B}
     if valu and "SQ_ACTIVE_INST_VALU" in valu:
         busy = 4.0 * valu["SQ_ACTIVE_INST_VALU"]        # SIMD-cycles with a VALU instruction issuing
         a = busy / kern_s / 1e12
@@ -486,9 +487,9 @@ def main():
             "evals_per_s": Bs * 10 / w_s, "batch": Bs, "kernel_avg_ms": k_s,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "bytes_per_eval": bpe,
-                         "traffic": tr["bytes_per_launch"] / Bs if tr else None,
+                         "traffic": tr["bytes_per_launch"] if tr else None,
                          "note": "the 65.5 MB exp(T) table is Infinity-Cache resident at C3, so "
-                                 "algorithmic bytes exceed HBM bytes (traffic = PMC HBM bytes per evaluation)"}}
+                                 "algorithmic bytes exceed HBM bytes (traffic = PMC HBM bytes per launch)"}}
         eng.set_option("score_path", PATHS[args.path])
         # fused per-step scorer of the sampler: 16 chains (C4 share of one GPU)
         from nemo.nem_order_mcmc import SIG0, SIG1
@@ -570,7 +571,7 @@ def main():
             ach = B * bpe / (kern_ms / 1e3) / 1e9
             tr = load_record("traffic.json", f"{args.config}:stream:b{B}", bid)
             roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] / B if tr else None,
+                    "frac": ach / HBM_PEAK_GBS, "traffic": tr["bytes_per_launch"] if tr else None,
                     "kernel": "score_kernel (streams exp(T) rows)", "kernel_avg_ms": kern_ms,
                     "kernel_avg_ms_launch_events": launch_ev_ms, "bytes_per_eval": bpe}
         roof["build_id"] = bid

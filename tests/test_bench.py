@@ -48,7 +48,7 @@ def test_roofline_is_a_hardware_fraction(monkeypatch):
         assert 0.0 < v["frac"] <= 1.0, k
     assert 0.25 < r["secondary"]["int8_mfma"]["frac"] < 0.4
     assert r["fp64_equivalent"]["vs_f64_mfma_peak"] > 1.0   # the note, not the headline
-    assert r["traffic"] == 66.6e6 / 2048
+    assert r["traffic"] == 66.6e6 and r["evals_per_launch"] == 2048   # HBM bytes per launch
     # without a record of this build: the live int8 matrix-core fraction
     monkeypatch.setattr(bench, "load_record", lambda name, key, bid: None)
     r = bench.score_roofline("C3", 64, 2000, 0, 2048, 10, 0.1466, 0.149, "y")
