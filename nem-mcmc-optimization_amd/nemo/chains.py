@@ -18,7 +18,7 @@ from scipy.linalg import inv
 from scipy.special import expit
 
 from .engine import Engine
-from .nem_order_mcmc import SIG0, SIG1, NEMOrderMCMC
+from .nem_order_mcmc import SIG0, SIG1, NEMOrderMCMC, draw_swap, permissible_batch, reset_weights_batch
 
 
 def shard(n_chains: int, rank: int, world: int) -> range:
@@ -55,28 +55,65 @@ def inv_stack(a):
     return out
 
 
-def _prepare_start(chains, pool=None):
+def propose_batch(chains, curr_perms, swap_prob=0.95, w=None):
+    """``get_new_order`` then ``reset(perm, i1, i2)`` (nem_order_mcmc.py:
+    231-255, :50-77) of every chain of a group: each chain draws from its own
+    stream in the reference's order, and the array work (the swap, positions,
+    permissible masks, the weight resets) runs once over the group's stacked
+    arrays.  Leaves every chain in the state its own calls would (same
+    arrays, same bits; its weights, positions and mask are views of the
+    group's stacks).  Returns the proposed orders and the stacks
+    (pos, weights, mask).  ``w``: a stack whose rows ARE the chains' current
+    weights (the last step's output); the reset then updates it in place, as
+    the reference updates ``self.parent_weights``."""
+    n = len(chains)
+    s = chains[0].num_s
+    ar = np.arange(n)
+    ij = np.array([draw_swap(c.rng, s, swap_prob) for c in chains], dtype=np.int64).reshape(n, 2)
+    perm = np.stack(curr_perms)
+    # i1, i2: the positions of the LABELS i, j in the current order
+    pos_c = np.empty_like(perm, dtype=np.int64)
+    pos_c[ar[:, None], perm] = np.arange(s)
+    i1, i2 = pos_c[ar, ij[:, 0]], pos_c[ar, ij[:, 1]]
+    # ...while the swap exchanges POSITIONS i, j (as written)
+    a, b = perm[ar, ij[:, 0]], perm[ar, ij[:, 1]]
+    perm[ar, ij[:, 0]], perm[ar, ij[:, 1]] = b, a
+    pos = np.empty((n, s), dtype=np.int64)
+    pos[ar[:, None], perm] = np.arange(s)
+    mask = permissible_batch(pos, chains[0].cap)
+    if w is None:
+        w = np.stack([c.parent_weights for c in chains])
+    reset_weights_batch(w, mask, i1, i2)
+    perms = list(perm)
+    for k, c in enumerate(chains):
+        c.ll = 0.0
+        c.parent_weights = w[k]
+        c._perm, c._pos, c._mask = perms[k], pos[k], mask[k]
+        c._parents = None
+    return perms, (pos, w, mask)
+
+
+def _prepare_start(chains, pool=None, stacks=None):
     """First half of ``_prepare``.  With an ``InvPool`` the per-chain work
-    (expit, inversion, clip) starts in its workers."""
-    pos = np.stack([c._pos for c in chains]).astype(np.int32)
+    (expit, inversion, clip) starts in its workers.  ``stacks``: the
+    group's (pos, weights, mask) stacks when they exist (propose_batch)."""
+    if stacks is None:
+        stacks = (np.stack([c._pos for c in chains]), np.stack([c.parent_weights for c in chains]),
+                  np.stack([c._mask for c in chains]))
+    pos, w, mask = stacks
+    pos = pos.astype(np.int32)
     if pool is not None:
-        pool.start_prepare([c.parent_weights for c in chains], [c._mask for c in chains])
-        return pos, None
-    w = np.stack([c.parent_weights for c in chains])
-    mask = np.stack([c._mask for c in chains])
+        pool.start_prepare(w, mask)
+        return pos, w, None
     sig = w.copy()
     sig[mask] = expit(w[mask])
     eye = np.identity(chains[0].num_s)
-    return pos, (w, sig, np.clip(inv_stack(eye - sig) - eye, 0, 1))
+    return pos, w, (sig, np.clip(inv_stack(eye - sig) - eye, 0, 1))
 
 
 def _prepare_end(chains, part, pool=None):
-    pos, rest = part
-    if rest is None:
-        w = np.stack([c.parent_weights for c in chains])
-        sig, anc = pool.finish_prepare()
-    else:
-        w, sig, anc = rest
+    pos, w, rest = part
+    sig, anc = pool.finish_prepare() if rest is None else rest
     for k, c in enumerate(chains):
         c.ll = 0.0
         c.ancestor_x = anc[k]
@@ -140,7 +177,7 @@ def opt_weights_batch(chains, engine: Engine, cap=0):
 
 
 def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, use_nem=False, cap=0,
-                raise_on_fail=True, pool=None, state=None, return_state=False):
+                raise_on_fail=True, pool=None, state=None, return_state=False, groups=None):
     """``NEMOrderMCMC.method`` (nem_order_mcmc.py:257-310) of every chain, in
     lock-step: each MCMC step is one fused device call per chain group.  Chain k
     draws from ``chains[k].rng`` in the reference's call order, and ends with
@@ -152,7 +189,8 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     ``raise_on_fail`` is set, the reference's Exception propagates and the
     chains' states are unspecified afterwards (see the pipeline below).
     ``pool`` (an ``InvPool``) runs the ancestor_x inversions in worker
-    processes; the results do not change."""
+    processes; the results do not change.  ``groups``: the number of chain
+    groups in the pipeline below (default 3 from 48 chains, else 2)."""
     n = len(chains)
     s = chains[0].num_s
     if state is None:
@@ -169,85 +207,107 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         st, curr = state["st"], state["curr"]
     props = [None] * n
 
-    def propose(idx):
-        for k in idx:
-            c = chains[k]
-            perm, i1, i2 = c.get_new_order(st[k]["curr_perm"], swap_prob=swap_prob)
-            c.reset(perm_order=perm, i1=i1, i2=i2)
-            props[k] = perm
+    def propose(idx, w=None):
+        perms, stacks = propose_batch([chains[k] for k in idx], [st[k]["curr_perm"] for k in idx],
+                                      swap_prob, w=w)
+        for j, k in enumerate(idx):
+            props[k] = perms[j]
+        return stacks
 
     def post(idx, lls):
         for j, k in enumerate(idx):
             c, q = chains[k], st[k]
             ll = float(lls[j])
             q["all_list"].append(ll)
-            dag = c.create_nem(c.parent_weights)[0] if use_nem else c.create_dag(c.parent_weights)[0]
             q["curr_list"].append(curr[k])
+            # the proposal's DAG (create_dag / create_nem, nem_order_mcmc.py:
+            # 210-221) is kept only when accepted: built after the draw
             acc, curr[k], q["curr_dag"], q["curr_perm"] = c.accepting(
-                ll, curr[k], gammas[k], dag, q["curr_dag"], props[k], q["curr_perm"])
+                ll, curr[k], gammas[k], None, q["curr_dag"], props[k], q["curr_perm"])
             q["acc"].append(acc)
-            if acc and curr[k] > q["best"]:
-                q["best"] = curr[k]
-                q["best_dag"] = dag
-                q["best_order"] = q["curr_perm"].copy()
-                q["best_parents"] = c.parents_list.copy()
-                q["best_struct"] = (c._pos, c._mask)
-                q["best_list"].append(q["best"])
-                q["best_order_list"].append(q["best_order"])
+            if acc:
+                dag = c.create_nem(c.parent_weights)[0] if use_nem else c.create_dag(c.parent_weights)[0]
+                q["curr_dag"] = dag
+                if curr[k] > q["best"]:
+                    q["best"] = curr[k]
+                    q["best_dag"] = dag
+                    q["best_order"] = q["curr_perm"].copy()
+                    q["best_parents"] = None   # parents_list of this order: built at the end
+                    q["best_perm"] = c._perm
+                    q["best_struct"] = (c._pos, c._mask)
+                    q["best_list"].append(q["best"])
+                    q["best_order_list"].append(q["best_order"])
 
-    # Two chain groups in a software pipeline: the device step of one group
-    # runs on the library's step thread (nemo_optimal_weights_begin / _end)
-    # while the host does the other group's accept / propose / reset /
-    # ancestor_x; the next group's step is queued before the running one
-    # ends, so the device goes from one group to the other without waiting
-    # for the host.
+    # Chain groups in a software pipeline: the device step of a group runs on
+    # the library's step thread (nemo_optimal_weights_begin / _end) while the
+    # host accepts / proposes / resets the others.  Per group: propose, hand
+    # its ancestor_x to the pool's workers, finish the oldest running group
+    # (its accept) while they compute, then queue this group's step.  With
+    # three or more groups one more step stays queued on the device while the
+    # host does that, so the device goes from group to group without waiting
+    # for the host; with two, the step is queued before the other one is
+    # finished instead.
     # Chains are independent and results are batch-invariant, so the bits are
     # those of one batch; use_nem scores on the device in the host phase, so it runs
     # unpipelined.  A failed local optimisation of one group surfaces when
-    # that group is finished, after the other group has already proposed its
+    # that group is finished, after others have already proposed their
     # next order: with raise_on_fail the exception leaves the chains' states
     # (orders, weights, RNG streams) unspecified -- only the results of runs
     # that complete are defined to equal a sequential batched run.
-    groups = [list(range(n))] if (use_nem or n < 2) else [list(range(n // 2)), list(range(n // 2, n))]
-    if len(groups) == 1:
+    n_groups = 1 if (use_nem or n < 2) else (groups or (3 if n >= 48 else 2))
+    n_groups = max(1, min(n_groups, n))
+    bounds = [n * g // n_groups for g in range(n_groups + 1)]
+    glist = [list(range(bounds[g], bounds[g + 1])) for g in range(n_groups)]
+    if n_groups == 1:
         for _ in range(n_iterations):
-            propose(groups[0])
-            post(groups[0], optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap,
-                                                  raise_on_fail=raise_on_fail, pool=pool))
+            propose(glist[0])
+            post(glist[0], optimal_weights_batch(chains, engine, use_nem=use_nem, cap=cap,
+                                                 raise_on_fail=raise_on_fail, pool=pool))
     else:
-        pending = None
+        from collections import deque
+        pending = deque()
+        wst = [None] * n_groups     # each group's weights stack (its last step's w_new)
+        early = n_groups >= 3       # finish the oldest group before queuing the next
 
-        def collect(p):
-            idx, cs, prep, call = p
+        def collect():
+            g, cs, prep, call = pending.popleft()
             call.end()
-            post(idx, _finish(cs, engine, prep, call.result(raise_on_fail), False, cap))
+            res = call.result(raise_on_fail)
+            wst[g] = res[0]
+            post(glist[g], _finish(cs, engine, prep, res, False, cap))
 
         try:
             for _ in range(n_iterations):
-                for idx in groups:
-                    propose(idx)
+                for g, idx in enumerate(glist):
+                    stacks = propose(idx, wst[g])
+                    wst[g] = None
                     cs = [chains[k] for k in idx]
-                    prep = _prepare_end(cs, _prepare_start(cs, pool), pool)
+                    part = _prepare_start(cs, pool, stacks)
+                    while early and len(pending) > n_groups - 2:
+                        collect()
+                    prep = _prepare_end(cs, part, pool)
                     pos, w, w01, anc = prep
                     call = engine.bind_optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
-                    # queued behind the other group's step: the device goes from
-                    # one group to the other while the host accepts the other
                     call.begin()
-                    p, pending = pending, (idx, cs, prep, call)
-                    if p is not None:
-                        collect(p)
-            p, pending = pending, None
-            if p is not None:
-                collect(p)
+                    pending.append((g, cs, prep, call))
+                    while len(pending) > n_groups - 1:
+                        collect()
+            while pending:
+                collect()
         finally:
-            if pending is not None:   # an exception left a queued step: wait for it
-                pending[3].end()
+            for p in pending:   # an exception left queued steps: wait for them
+                p[3].end()
     for k, c in enumerate(chains):
         q = st[k]
         c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]
         c.all_score_list, c.curr_score_list = q["all_list"], q["curr_list"]
         c.best_score_list, c.best_order_list = q["best_list"], q["best_order_list"]
         c.accepted = q["acc"]
+        if q["best_parents"] is None:
+            bpos = q["best_struct"][0]
+            q["best_parents"] = np.empty(s, dtype=object)
+            for i in range(s):
+                q["best_parents"][i] = c._parents_of(q["best_perm"], bpos, i)
         c.parents_list = q["best_parents"]
         c._pos, c._mask = q["best_struct"]
     best = np.array([q["best"] for q in st])
@@ -269,7 +329,7 @@ class ChainBatch:
     ancestor_x inversions in worker processes: same bits, less host time."""
 
     def __init__(self, nem, init_orders, seeds, engine: Engine | None = None, gamma=None,
-                 swap_prob=0.95, use_nem=False, cap=0, on_fail="raise", inv_pool=None):
+                 swap_prob=0.95, use_nem=False, cap=0, on_fail="raise", inv_pool=None, groups=None):
         if on_fail not in ("raise", "continue"):
             raise ValueError(f"on_fail={on_fail!r}: 'raise' or 'continue'")
         self.raise_on_fail = on_fail == "raise"
@@ -284,6 +344,7 @@ class ChainBatch:
         if inv_pool is not None and (inv_pool.s != nem.num_s or inv_pool.maxb < len(init_orders)):
             raise ValueError("inv_pool: matrix size or capacity does not fit this batch")
         self.inv_pool = inv_pool
+        self.groups = groups      # pipeline chain groups (run_methods); None: by batch size
         self._state = None
         self.chains = []
         for order, seed in zip(init_orders, seeds):
@@ -304,7 +365,7 @@ class ChainBatch:
         self.best_scores, self._state = run_methods(
             self.chains, self.gammas, n_iterations, self.engine, swap_prob=self.swap_prob, use_nem=self.use_nem,
             cap=self.cap, raise_on_fail=self.raise_on_fail, pool=self.inv_pool,
-            state=self._state if resume else None, return_state=True)
+            state=self._state if resume else None, return_state=True, groups=self.groups)
         self.best_orders = [np.asarray(c.best_order).copy() for c in self.chains]
         self.accepted = np.array([c.accepted for c in self.chains]).T.reshape(-1, self.n)
         return self.best_scores, np.stack(self.best_orders)

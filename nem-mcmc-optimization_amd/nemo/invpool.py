@@ -144,9 +144,8 @@ class InvPool:
     def start_prepare(self, ws, masks):
         n = len(ws)
         self._check(n)
-        for k in range(n):
-            self._a[k] = ws[k]
-            self._m[k] = masks[k]
+        self._a[:n] = ws
+        self._m[:n] = masks
         self._send("prep", n)
 
     def _drain(self):

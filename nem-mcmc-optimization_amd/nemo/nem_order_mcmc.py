@@ -36,6 +36,49 @@ SIG0 = float(expit(0.0))   # expit of a binarised "no edge" weight
 SIG1 = float(expit(1.0))   # expit of a binarised "edge" weight
 
 
+def draw_swap(rng, s, swap_prob=0.95):
+    """The draws of get_new_order (nem_order_mcmc.py:236-241): one random(),
+    then a sample of two positions or one randint (adjacent swap)."""
+    if rng.random() < swap_prob:
+        i, j = rng.sample(range(s), 2)
+    else:
+        i = rng.randint(0, s - 2)
+        j = i + 1
+    return i, j
+
+
+def permissible_batch(pos, cap=0):
+    """mask[c, i, j]: j is a permissible parent of i in order c (it comes
+    before i, within ``cap`` places when a cap is set)."""
+    p = pos.astype(np.int16)            # S <= 32767: the gaps fit
+    m = p[:, :, None] > p[:, None, :]
+    if cap:
+        m &= (p[:, :, None] - p[:, None, :]) <= cap
+    return m
+
+
+def reset_weights_batch(w, mask, i1, i2, init_value=0.5):
+    """``get_permissible_parents(init=False)``'s in-place weight updates
+    (nem_order_mcmc.py:67-77; the per-chain form is
+    NEMOrderMCMC.get_permissible_parents) on a stack of chains at once:
+    w[c], mask[c] of chain c with its own i1[c], i2[c] (i1 != i2).  Rows and
+    columns i1, i2 are zeroed; then column i1 holds ``init_value`` at the
+    children with i1 as a permissible parent, column i2 at the remaining
+    children with i2 as one, and column i (i in {i1, i2}) additionally at
+    i's own parents when i is in neither set.  Every write stores one of two
+    constants, so the order of the reference's writes fixes the result."""
+    n = w.shape[0]
+    ar = np.arange(n)
+    w[ar, i1] = 0
+    w[ar, i2] = 0
+    to1 = mask[ar, :, i1]                 # (n, S): mask[c, :, i1[c]]
+    to2 = mask[ar, :, i2] & ~to1
+    for i, col in ((i1, to1), (i2, to2)):
+        quirk = ~to1[ar, i] & ~to2[ar, i]
+        col = col | (mask[ar, i, :] & quirk[:, None])
+        w[ar, :, i] = np.where(col, init_value, 0.0)
+
+
 class NEMOrderMCMC:
     # proposal / acceptance stream: the global ``random`` module, as in the
     # reference; nemo.chains gives each batched chain its own random.Random
@@ -297,12 +340,7 @@ class NEMOrderMCMC:
         """Reference: nem_order_mcmc.py:231-255.  i1, i2 are the positions of
         the node LABELS i, j; the swap exchanges POSITIONS i, j (as written)."""
         perm_order = curr_perm_order.copy()
-        rng = self.rng
-        if rng.random() < swap_prob:
-            i, j = rng.sample(range(self.num_s), 2)
-        else:
-            i = rng.randint(0, self.num_s - 2)
-            j = i + 1
+        i, j = draw_swap(self.rng, self.num_s, swap_prob)
         i1 = np.where(perm_order == i)[0][0]
         i2 = np.where(perm_order == j)[0][0]
         perm_order[i], perm_order[j] = perm_order[j], perm_order[i]

@@ -270,20 +270,33 @@ def test_chain_batch_equals_single_chains():
     from nemo.chains import ChainBatch
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m = generator.synthetic_nem(16, 500, 0)
-    orders = [np.random.default_rng(k).permutation(16) for k in range(4)]
-    seeds = [11, 12, 13, 14]
+    nc = 7
+    orders = [np.random.default_rng(k).permutation(16) for k in range(nc)]
+    seeds = [11 + k for k in range(nc)]
     cb = ChainBatch(m, orders, seeds, swap_prob=0.95)
     best, best_orders = cb.run(8)
-    for k in range(4):
+    for k in range(nc):
         single = NEMOrderMCMC(m, orders[k], engine=cb.engine)
         single.rng = random.Random(seeds[k])
         b, _ = single.method(n_iterations=8, gamma=cb.gamma, swap_prob=0.95, verbose=False)
         assert np.array_equal(np.array(single.accepted), cb.accepted[:, k])
         assert b == best[k]
         assert np.array_equal(single.best_order, best_orders[k])
+        c = cb.chains[k]
+        assert np.array_equal(single.best_dag, c.best_dag) and single.best_dag.dtype == c.best_dag.dtype
+        assert single.all_score_list == c.all_score_list and single.curr_score_list == c.curr_score_list
+        assert single.best_score_list == c.best_score_list
+        assert all(np.array_equal(x, y) for x, y in zip(single.parents_list, c.parents_list))
+        assert np.array_equal(single.parent_weights, c.parent_weights)
+    # three pipeline groups, one group: the same trajectories
+    for g in (3, 1):
+        cbg = ChainBatch(m, orders, seeds, swap_prob=0.95, engine=cb.engine, groups=g)
+        bg, bog = cbg.run(8)
+        assert np.array_equal(bg, best) and np.array_equal(bog, best_orders)
+        assert np.array_equal(cbg.accepted, cb.accepted)
     # ancestor_x inversions in worker processes: the same trajectories
     from nemo.invpool import InvPool
-    pool = InvPool(16, 4, n_workers=2)
+    pool = InvPool(16, nc, n_workers=2)
     try:
         cbp = ChainBatch(m, orders, seeds, swap_prob=0.95, engine=cb.engine, inv_pool=pool)
         bp, bop = cbp.run(8)

@@ -20,10 +20,12 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--local-prod", type=int, default=1)
+    ap.add_argument("--local-wpb", type=int, default=0, help="option local_wpb (0: library default)")
     ap.add_argument("--seed-base", type=int, default=1234)
     ap.add_argument("--on-fail", default="continue", choices=["raise", "continue"])
     ap.add_argument("--inv-workers", type=int, default=0, help="InvPool worker processes (0: serial inv)")
     ap.add_argument("--timeline", action="store_true", help="print per-phase timestamps of 3 steps")
+    ap.add_argument("--groups", type=int, default=0, help="pipeline chain groups (0: ChainBatch default)")
     a = ap.parse_args()
     from nemo import generator, utils
     from nemo.chains import ChainBatch
@@ -34,9 +36,11 @@ def main():
     cb = ChainBatch(m, [order] * a.chains, seeds=[a.seed_base + c for c in range(a.chains)],
                     on_fail=a.on_fail, inv_pool=pool)
     cb.engine.set_option("local_prod", a.local_prod)
+    if a.local_wpb:
+        cb.engine.set_option("local_wpb", a.local_wpb)
     cb.run(2)  # warm-up
     cb = ChainBatch(m, [order] * a.chains, seeds=[a.seed_base + c for c in range(a.chains)], engine=cb.engine,
-                    on_fail=a.on_fail, inv_pool=pool)
+                    on_fail=a.on_fail, inv_pool=pool, groups=a.groups or None)
     marks = []
     if a.timeline:
         import threading
@@ -66,7 +70,7 @@ def main():
     if prof:
         prof.disable()
     dt = time.perf_counter() - t0
-    print(f"{a.config}: {a.chains} chains x {a.steps} steps in {dt:.3f} s: "
+    print(f"{a.config}: groups {a.groups or 'default'}, {a.chains} chains x {a.steps} steps in {dt:.3f} s: "
           f"{1e3 * dt / a.steps:.2f} ms/step, {a.chains * a.steps / dt:.0f} chain-steps/s; best {best.max():.3f}")
     if marks:
         marks.sort()
