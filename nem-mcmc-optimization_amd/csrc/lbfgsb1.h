@@ -117,12 +117,20 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
       stpf = stpmin;
     }
   }
-  if (fp > fx) {
-    sty = stp; fy = fp; dy = dp;
-  } else {
-    if (sgnd < 0.0) { sty = stx; fy = fx; dy = dx; }
-    stx = stp; fx = fp; dx = dp;
-  }
+  // the interval update as value selects: written as branches that assign
+  // either end, the compiler kept (stx, fx, dx, sty, fy, dy) in a scratch
+  // array with computed store addresses -- a chain of scratch round trips in
+  // every line-search step, most of a lone wave's time per f-evaluation
+  const bool upper = fp > fx;
+  const bool swap = !upper && sgnd < 0.0;
+  const double nsty = upper ? stp : (swap ? stx : sty);
+  const double nfy = upper ? fp : (swap ? fx : fy);
+  const double ndy = upper ? dp : (swap ? dx : dy);
+  const double nstx = upper ? stx : stp;
+  const double nfx = upper ? fx : fp;
+  const double ndx = upper ? dx : dp;
+  sty = nsty; fy = nfy; dy = ndy;
+  stx = nstx; fx = nfx; dx = ndx;
   stp = stpf;
 }
 

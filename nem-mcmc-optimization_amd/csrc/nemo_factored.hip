@@ -114,8 +114,10 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
     const double* __restrict__ e_lo, const double* __restrict__ e_hi, double* __restrict__ Dp,
     double* __restrict__ G, int32_t* __restrict__ permo) {
   __shared__ int perm[kMaxS];
-  // block = (evaluation, group of 16 child positions); 4 waves x 4 rows
-  const int ngroups = SPAD / 16;
+  // block = (evaluation, group of 4 child positions); one row per wave (the
+  // rows of one evaluation spread over SPAD / 4 blocks: a lone evaluation's
+  // prep is a quarter of the serial work per wave it was with 16-row blocks)
+  const int ngroups = SPAD / 4;
   const int b = blockIdx.x / ngroups;
   const int grp = blockIdx.x - b * ngroups;
   const int tid = threadIdx.x;
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
   if (grp == 0)
     for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
   const int nw = blockDim.x / kWave;
-  for (int q = 16 * grp + w; q < 16 * grp + 16; q += nw) {
+  for (int q = 4 * grp + w; q < 4 * grp + 4; q += nw) {
     const int i = q < S ? perm[q] : 0;
     const double* wrow = w01 + ((size_t)b * S + i) * S;
     double* drow = Dp + ((size_t)b * SPAD + q) * SPAD;
@@ -601,7 +603,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const bool pipe = fk == 2 || fk == 3;
   hipError_t err = hipSuccess;
   if (!i8 && !i8o && !win && !wide) {  // the int8 and lookup-table kernels derive their inputs themselves
-    prep_factored_kernel<<<batch * (spad / 16), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
+    prep_factored_kernel<<<batch * (spad / 4), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
   }

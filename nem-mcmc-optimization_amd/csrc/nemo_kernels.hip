@@ -406,10 +406,24 @@ struct LocalObjective {
   double c[NPL];  // this lane's share of the c vector, kept in registers
   double anc;
   const double2* ltab;  // log_fast table (LDS)
+#ifdef NEMO_LO_TRACE
+  // cycle probe: a build with -DNEMO_LO_TRACE=<nfev> prints, for every pair
+  // needing at least that many f-evaluations, the cycles of its minimisation
+  // and of the objective's parts (expit, products, log + wave sums); run
+  // tools/lo_stats.py with NEMO_LIBRARY pointing at that build
+  mutable long long cy_exp = 0, cy_prod = 0, cy_tail = 0, cy_calls = 0;
+#endif
   __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
 #pragma clang fp contract(off)
+#ifdef NEMO_LO_TRACE
+    const long long t0 = clock64();
+#endif
     const double e0 = expit_d(x0);
     const double e1 = expit_d(x1);
+#ifdef NEMO_LO_TRACE
+    const long long te = clock64();
+    long long tp = te;
+#endif
     double p0 = 0.0, p1 = 0.0;
     if constexpr (PROD) {
       constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;
@@ -448,6 +462,10 @@ struct LocalObjective {
       k0 += __builtin_amdgcn_frexp_exp(m0[0]);
       k1 += __builtin_amdgcn_frexp_exp(m1[0]);
       const double r0 = __builtin_amdgcn_frexp_mant(m0[0]), r1 = __builtin_amdgcn_frexp_mant(m1[0]);
+#ifdef NEMO_LO_TRACE
+      __builtin_amdgcn_s_waitcnt(0);
+      tp = clock64();
+#endif
       p0 = fma((double)k0, kLn2Hi, log_fast(r0, ltab)) + (double)k0 * kLn2Lo;
       p1 = fma((double)k1, kLn2Hi, log_fast(r1, ltab)) + (double)k1 * kLn2Lo;
     } else {
@@ -465,6 +483,13 @@ struct LocalObjective {
     // nem_order_mcmc.py:20-22: (-sum + |ex - anc|) + ex*(1 - ex)
     f0 = (-p0 + fabs(e0 - anc)) + e0 * (1.0 - e0);
     f1 = (-p1 + fabs(e1 - anc)) + e1 * (1.0 - e1);
+#ifdef NEMO_LO_TRACE
+    const long long t3 = clock64();
+    cy_exp += te - t0;
+    cy_prod += tp - te;
+    cy_tail += t3 - tp;
+    cy_calls += 1;
+#endif
   }
 };
 
@@ -523,7 +548,16 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
     obj.c[q] = (e < E) ? local_c((double)tv[e], owk[e], s) : 0.0;  // padding: log(1) = 0
   }
   obj.anc = anc[idx];
+#ifdef NEMO_LO_TRACE
+  const long long ts = clock64();
+#endif
   const LbfgsResult r = lbfgsb1_minimize(obj, s);
+#ifdef NEMO_LO_TRACE
+  const long long tend = clock64();
+  if (lane == 0 && r.nfev >= NEMO_LO_TRACE)
+    printf("lo_trace b %d i %d k %d nfev %d nit %d min %lld calls %lld exp %lld prod %lld tail %lld\n", b, i, k,
+           r.nfev, r.nit, tend - ts, obj.cy_calls, obj.cy_exp, obj.cy_prod, obj.cy_tail);
+#endif
   if (lane == 0) {
     const double wx = expit_d(r.x);
     wnew[idx] = wx;

@@ -24,10 +24,16 @@ rng = np.random.default_rng(3)
 pos = np.array([rng.permutation(S) for _ in range(n)], dtype=np.int32)
 w = rng.uniform(-3, 3, (n, S, S))
 anc = np.clip(rng.random((n, S, S)) - 0.5, 0, 1)
-_, _, _, info = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
+w_new, ll1, lld, info = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
+import hashlib  # noqa: E402
+print("sha256(w_new, ll1, lld, info)", hashlib.sha256(b"".join(np.ascontiguousarray(a).tobytes()
+                                                         for a in (w_new, ll1, lld, info))).hexdigest()[:16])
 inf = info[info != -1]
 nit, nfev, st = (inf >> 4) & 4095, (inf >> 16) & 32767, inf & 15
 for name, v in (("nit", nit), ("nfev", nfev)):
     q = np.percentile(v, [50, 90, 99, 100])
     print(f"{name}: mean {v.mean():.2f} p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f}")
-print("status counts", np.bincount(st, minlength=4).tolist(), "pairs", inf.size)
+print("status counts", np.bincount(st, minlength=4).tolist(), "pairs", inf.size, "sum nfev", int(nfev.sum()))
+# repeated launches of the same step for a counter pass (rocprofv3 --pmc)
+for _ in range(int(os.environ.get("LO_REPEAT", "0"))):
+    eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)

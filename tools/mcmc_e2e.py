@@ -20,7 +20,6 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--local-prod", type=int, default=1)
-    ap.add_argument("--local-wpb", type=int, default=0, help="option local_wpb (0: library default)")
     ap.add_argument("--seed-base", type=int, default=1234)
     ap.add_argument("--on-fail", default="continue", choices=["raise", "continue"])
     ap.add_argument("--inv-workers", type=int, default=0, help="InvPool worker processes (0: serial inv)")
@@ -36,8 +35,6 @@ def main():
     cb = ChainBatch(m, [order] * a.chains, seeds=[a.seed_base + c for c in range(a.chains)],
                     on_fail=a.on_fail, inv_pool=pool)
     cb.engine.set_option("local_prod", a.local_prod)
-    if a.local_wpb:
-        cb.engine.set_option("local_wpb", a.local_wpb)
     cb.run(2)  # warm-up
     cb = ChainBatch(m, [order] * a.chains, seeds=[a.seed_base + c for c in range(a.chains)], engine=cb.engine,
                     on_fail=a.on_fail, inv_pool=pool, groups=a.groups or None)
