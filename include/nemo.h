@@ -137,13 +137,15 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
                              double* d_ll1, double* d_ll_dag, int32_t* d_info, void* stream);
 /* nemo_optimal_weights as a queued call: _begin checks the context and
  * pointers and returns at once; a library thread runs the queued calls in
- * order (transfers, launches, the NEMO_ERR_OPT check); _end waits for the
+ * order (transfers, launches, the NEMO_ERR_OPT check), two in flight at a
+ * time: it stages and queues the next call's device work before it waits for
+ * the previous one, so the device runs them back to back; _end waits for the
  * oldest call not yet ended and returns its result code (nemo_last_error()
  * then holds its message).  The caller keeps every buffer alive and untouched
  * until the matching _end, and makes no other call on ctx in between except
  * further _begin / _end.  Replaces, like nemo_optimal_weights,
  * get_optimal_weights(init=True) (nem_order_mcmc.py:172-208) for a caller
- * that runs two chain groups in a pipeline (nemo/chains.py). */
+ * that runs chain groups in a pipeline (nemo/chains.py). */
 int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
                                const double* anc, double sig0, double sig1, int cap, double* w_new,
                                double* ll1, double* ll_dag, int32_t* info);

@@ -26,6 +26,7 @@ struct StepJob {
   int32_t* info;
   int rc = 0;
   std::string err;
+  int slot = 0;  // staging slot while in flight
 };
 
 struct nemo_ctx {
@@ -142,10 +143,14 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_step, c.d_nullsum_w};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
-  if (c.h_stage) (void)hipHostFree(c.h_stage);
+  for (int k = 0; k < Ctx::kStepSlots; ++k) {
+    if (c.h_stage[k]) (void)hipHostFree(c.h_stage[k]);
+    if (c.d_step[k]) (void)hipFree(c.d_step[k]);
+    if (c.step_done[k]) (void)hipEventDestroy(c.step_done[k]);
+  }
   for (hipEvent_t ev : c.ev_pool) (void)hipEventDestroy(ev);
   for (auto& g : c.step_graph)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -198,33 +203,21 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
 
 namespace {
 
-// grow the pinned host staging buffer to at least `bytes`
-int host_stage(Ctx& c, size_t bytes) {
-  if (bytes <= c.h_stage_bytes) return NEMO_OK;
+// grow staging slot `slot` (pinned host buffer and its device mirror) to at
+// least `bytes`
+int step_stage(Ctx& c, int slot, size_t bytes) {
+  if (!c.step_done[slot]) HIPCHK(hipEventCreateWithFlags(&c.step_done[slot], hipEventDisableTiming));
+  if (bytes <= c.h_stage_bytes[slot] && bytes <= c.d_step_bytes[slot]) return NEMO_OK;
   ++c.graph_epoch;
   HIPCHK(hipStreamSynchronize(c.stream));
-  if (c.h_stage) {
-    HIPCHK(hipHostFree(c.h_stage));
-    c.h_stage = nullptr;
-    c.h_stage_bytes = 0;
-  }
-  HIPCHK(hipHostMalloc(&c.h_stage, bytes, hipHostMallocDefault));
-  c.h_stage_bytes = bytes;
-  return NEMO_OK;
-}
-
-// grow the device block that mirrors the staging layout to at least `bytes`
-int dev_stage(Ctx& c, size_t bytes) {
-  if (bytes <= c.d_step_bytes) return NEMO_OK;
-  ++c.graph_epoch;
-  HIPCHK(hipStreamSynchronize(c.stream));
-  if (c.d_step) {
-    HIPCHK(hipFree(c.d_step));
-    c.d_step = nullptr;
-    c.d_step_bytes = 0;
-  }
-  HIPCHK(hipMalloc(&c.d_step, bytes));
-  c.d_step_bytes = bytes;
+  if (c.h_stage[slot]) HIPCHK(hipHostFree(c.h_stage[slot]));
+  if (c.d_step[slot]) HIPCHK(hipFree(c.d_step[slot]));
+  c.h_stage[slot] = c.d_step[slot] = nullptr;
+  c.h_stage_bytes[slot] = c.d_step_bytes[slot] = 0;
+  HIPCHK(hipHostMalloc(&c.h_stage[slot], bytes, hipHostMallocDefault));
+  c.h_stage_bytes[slot] = bytes;
+  HIPCHK(hipMalloc(&c.d_step[slot], bytes));
+  c.d_step_bytes[slot] = bytes;
   return NEMO_OK;
 }
 
@@ -632,58 +625,69 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
   return NEMO_OK;
 }
 
-int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
-                         const double* anc, double sig0, double sig1, int cap, double* w_new,
-                         double* ll1, double* ll_dag, int32_t* info) {
+// every transfer of a fused step goes through a pinned staging slot: [pos |
+// w01 | anc | w_new | info | ll1 | ll_dag], each part 256-B aligned, and a
+// device block with the same layout: one H2D of [pos .. info] (info preset to
+// -1 = not a permissible pair) and one D2H of [w_new .. ll_dag]
+struct StepLayout {
+  size_t o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, total;
+  StepLayout(size_t S, size_t n) {
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    o_w01 = up(n * S * 4);
+    o_anc = o_w01 + up(n * S * S * 8);
+    o_wn = o_anc + up(n * S * S * 8);
+    o_inf = o_wn + up(n * S * S * 8);
+    o_ll1 = o_inf + up(n * S * S * 4);
+    o_lld = o_ll1 + up(n * 8);
+    total = o_lld + up(n * 8);
+  }
+};
+
+// first half of nemo_optimal_weights: validate, fill staging slot `slot`,
+// queue the device work (one H2D copy, the launches, one D2H copy) and record
+// the slot's event; returns without waiting
+static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, const double* w01,
+                      const double* anc, double sig0, double sig1, int cap, const double* w_new) {
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
   if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
   if (nchains == 0) return NEMO_OK;
-  if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  if (!pos || !w01 || !anc || !w_new) return fail(NEMO_ERR_ARG, "null host pointer");
   Ctx& c = ctx->c;
   if ((rc = check_pos(pos, nchains, c.S))) return rc;
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
   const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
-  // every transfer goes through the pinned staging buffer: [pos | w01 | anc |
-  // w_new | info | ll1 | ll_dag], each part 256-B aligned, and a device block
-  // with the same layout: one H2D of [pos .. info] (info preset to -1 = not a
-  // permissible pair) and one D2H of [w_new .. ll_dag]
-  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t o_w01 = up(n * S * 4), o_anc = o_w01 + up(n * S * S * 8), o_wn = o_anc + up(n * S * S * 8),
-               o_inf = o_wn + up(n * S * S * 8), o_ll1 = o_inf + up(n * S * S * 4), o_lld = o_ll1 + up(n * 8),
-               total = o_lld + up(n * 8);
-  if ((rc = host_stage(c, total))) return rc;
-  if ((rc = dev_stage(c, total))) return rc;
-  char* hs = (char*)c.h_stage;
-  char* ds = (char*)c.d_step;
+  const StepLayout L(S, n);
+  if ((rc = step_stage(c, slot, L.total))) return rc;
+  char* hs = (char*)c.h_stage[slot];
+  char* ds = (char*)c.d_step[slot];
   memcpy(hs, pos, n * S * 4);
-  memcpy(hs + o_w01, w01, n * S * S * 8);
-  memcpy(hs + o_anc, anc, n * S * S * 8);
-  memcpy(hs + o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
-  memset(hs + o_inf, 0xff, n * S * S * 4);
-  // the device work: one H2D copy of [pos .. info], the launches, one D2H copy
-  // of [w_new .. ll_dag]; replayed as a hipGraph per (nchains, cap) while no
-  // captured argument changes (the staging buffers, options and tables bump
+  memcpy(hs + L.o_w01, w01, n * S * S * 8);
+  memcpy(hs + L.o_anc, anc, n * S * S * 8);
+  memcpy(hs + L.o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
+  memset(hs + L.o_inf, 0xff, n * S * S * 4);
+  // replayed as a hipGraph per (nchains, cap, slot) while no captured
+  // argument changes (the staging buffers, options and tables bump
   // graph_epoch), so a step costs one graph launch instead of ~10 API calls
   auto enqueue = [&]() -> int {
-    HIPCHK(hipMemcpyAsync(ds, hs, o_ll1, hipMemcpyHostToDevice, st));
-    int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + o_w01),
-                                     (const double*)(ds + o_anc), sig0, sig1, cap, (double*)(ds + o_wn),
-                                     (double*)(ds + o_ll1), (double*)(ds + o_lld), (int32_t*)(ds + o_inf), st);
+    HIPCHK(hipMemcpyAsync(ds, hs, L.o_ll1, hipMemcpyHostToDevice, st));
+    int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
+                                     (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
+                                     (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st);
     if (r) return r;
-    HIPCHK(hipMemcpyAsync(hs + o_wn, ds + o_wn, total - o_wn, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(hs + L.o_wn, ds + L.o_wn, L.total - L.o_wn, hipMemcpyDeviceToHost, st));
     return NEMO_OK;
   };
   Ctx::StepGraph* sg = nullptr;
   if (c.graphs && !c.timing) {
     for (auto& g : c.step_graph)
-      if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.sig0 == sig0 &&
-          g.sig1 == sig1)
+      if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.slot == slot &&
+          g.sig0 == sig0 && g.sig1 == sig1)
         sg = &g;
     if (!sg) {  // capture once
       Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
-      c.step_graph_next = (c.step_graph_next + 1) % 4;
+      c.step_graph_next = (c.step_graph_next + 1) % Ctx::kStepGraphs;
       if (g.exec) {
         (void)hipGraphExecDestroy(g.exec);
         g.exec = nullptr;
@@ -696,6 +700,7 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
             hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0) == hipSuccess) {
           g.nchains = nchains;
           g.cap = cap;
+          g.slot = slot;
           g.sig0 = sig0;
           g.sig1 = sig1;
           g.epoch = c.graph_epoch;
@@ -717,12 +722,25 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
   } else if ((rc = enqueue())) {
     return rc;
   }
-  HIPCHK(hipStreamSynchronize(st));
-  memcpy(w_new, hs + o_wn, n * S * S * 8);
-  memcpy(ll1, hs + o_ll1, n * 8);
-  memcpy(ll_dag, hs + o_lld, n * 8);
-  if (info) memcpy(info, hs + o_inf, n * S * S * 4);
-  const int32_t* inf = (const int32_t*)(hs + o_inf);
+  HIPCHK(hipEventRecord(c.step_done[slot], st));
+  return NEMO_OK;
+}
+
+// second half: wait for the slot's device work, hand the outputs back and
+// raise the reference's error for a failed local optimisation
+static int step_finish(nemo_ctx* ctx, int slot, int nchains, double* w_new, double* ll1, double* ll_dag,
+                       int32_t* info) {
+  Ctx& c = ctx->c;
+  if (nchains == 0) return NEMO_OK;
+  const size_t S = c.S, n = nchains;
+  const StepLayout L(S, n);
+  HIPCHK(hipEventSynchronize(c.step_done[slot]));
+  const char* hs = (const char*)c.h_stage[slot];
+  memcpy(w_new, hs + L.o_wn, n * S * S * 8);
+  memcpy(ll1, hs + L.o_ll1, n * 8);
+  memcpy(ll_dag, hs + L.o_lld, n * 8);
+  if (info) memcpy(info, hs + L.o_inf, n * S * S * 4);
+  const int32_t* inf = (const int32_t*)(hs + L.o_inf);
   for (size_t k = 0; k < n * S * S; ++k) {
     if (inf[k] == -1) continue;  // not a permissible pair
     const int status = inf[k] & 15;
@@ -737,8 +755,20 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
   return NEMO_OK;
 }
 
+int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
+                         const double* anc, double sig0, double sig1, int cap, double* w_new,
+                         double* ll1, double* ll_dag, int32_t* info) {
+  if (!ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  int rc = step_start(ctx, 0, nchains, pos, w01, anc, sig0, sig1, cap, w_new);
+  if (rc) return rc;
+  return step_finish(ctx, 0, nchains, w_new, ll1, ll_dag, info);
+}
+
 // asynchronous form: the library thread runs each call's transfers, launches
-// and checks; the caller's thread only queues and, later, collects
+// and checks; the caller's thread only queues and, later, collects.  Two calls
+// are in flight at once (staging slots 1 and 2): the thread stages and queues
+// the next call while the device still runs the previous one, then waits for
+// that one (nemo_host.h StepQueue)
 int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
                                const double* anc, double sig0, double sig1, int cap, double* w_new,
                                double* ll1, double* ll_dag, int32_t* info) {
@@ -748,12 +778,28 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
   if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
   std::string err;
   try {
-    if (!ctx->steps)
-      ctx->steps.reset(new nemo::host::StepQueue<StepJob>([ctx](StepJob& j) {
-        j.rc = nemo_optimal_weights(ctx, j.nchains, j.pos, j.w01, j.anc, j.sig0, j.sig1, j.cap, j.w_new, j.ll1,
-                                    j.ll_dag, j.info);
-        if (j.rc) j.err = g_err;
-      }));
+    if (!ctx->steps) {
+      auto next_slot = std::make_shared<int>(1);
+      ctx->steps.reset(new nemo::host::StepQueue<StepJob>(
+          [ctx, next_slot](StepJob& j) {  // start: true = in flight
+            j.slot = *next_slot;
+            j.rc = step_start(ctx, j.slot, j.nchains, j.pos, j.w01, j.anc, j.sig0, j.sig1, j.cap, j.w_new);
+            if (j.rc) {
+              j.err = g_err;
+              (void)hipStreamSynchronize(ctx->c.stream);  // nothing of it left running in its slot
+              return false;
+            }
+            if (j.nchains == 0) return false;
+            *next_slot = 3 - *next_slot;
+            return true;
+          },
+          [ctx](StepJob& j) { return hipEventQuery(ctx->c.step_done[j.slot]) != hipErrorNotReady; },
+          [ctx](StepJob& j) {
+            j.rc = step_finish(ctx, j.slot, j.nchains, j.w_new, j.ll1, j.ll_dag, j.info);
+            if (j.rc) j.err = g_err;
+          },
+          2));
+    }
     std::unique_ptr<StepJob> j(new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info});
     if (ctx->steps->submit(std::move(j), &err)) return NEMO_OK;
   } catch (const std::exception& e) {

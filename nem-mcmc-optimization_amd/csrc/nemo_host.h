@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <deque>
@@ -264,11 +265,31 @@ inline bool build_inverse_schedule(InverseSchedule& sch, int S, int nprob, const
 // back.  The destructor lets every job already submitted run to completion
 // (their callers' output buffers are written even if never collected), then
 // stops the worker; jobs not collected by then are freed.
+//
+// Two forms.  StepQueue(run): the worker runs each job to completion in turn.
+// StepQueue(start, ready, finish, depth): a job is started (queued on the
+// device; true = in flight, false = already complete, e.g. failed), and up to
+// `depth` jobs are in flight at once; the oldest is finished (waited for,
+// outputs handed back) when no further job can start, as soon as ready()
+// reports its device work done -- so a job submitted while the device still
+// runs the previous one is started before that one is waited for, and the
+// device goes from one job to the next without waiting for the host.
 template <class Job>
 class StepQueue {
  public:
   using Runner = std::function<void(Job&)>;
-  explicit StepQueue(Runner run) : run_(std::move(run)) {}
+  using Start = std::function<bool(Job&)>;
+  using Ready = std::function<bool(Job&)>;
+  using Finish = std::function<void(Job&)>;
+  explicit StepQueue(Runner run)
+      : start_([run](Job& j) {
+          run(j);
+          return false;
+        }),
+        depth_(1) {}
+  StepQueue(Start start, Ready ready, Finish finish, int depth)
+      : start_(std::move(start)), ready_(std::move(ready)), finish_(std::move(finish)),
+        depth_(depth < 1 ? 1 : depth) {}
   StepQueue(const StepQueue&) = delete;
   StepQueue& operator=(const StepQueue&) = delete;
   ~StepQueue() { shutdown(); }
@@ -309,7 +330,7 @@ class StepQueue {
     cv_.wait(lk, [this] { return jobs_.front().done; });
     std::unique_ptr<Job> j = std::move(jobs_.front().job);
     jobs_.pop_front();
-    --next_run_;
+    --next_start_;
     return j;
   }
 
@@ -329,7 +350,7 @@ class StepQueue {
     if (worker_.joinable()) worker_.join();
     std::lock_guard<std::mutex> g(mu_);
     jobs_.clear();
-    next_run_ = 0;
+    next_start_ = 0;
   }
 
  private:
@@ -337,29 +358,69 @@ class StepQueue {
     std::unique_ptr<Job> job;
     bool done;
   };
+  static constexpr int kPollUs = 20;  // in-flight job's readiness poll while no new job is queued
+
+  void mark_done(Job* j) {  // under mu_
+    for (auto& e : jobs_)
+      if (e.job.get() == j) {
+        e.done = true;
+        break;
+      }
+    cv_.notify_all();
+  }
 
   void loop() {
     std::unique_lock<std::mutex> lk(mu_);
+    std::deque<Job*> flying;  // started, not finished, oldest first
     for (;;) {
-      cv_.wait(lk, [this] { return stop_ || next_run_ < jobs_.size(); });
-      if (next_run_ >= jobs_.size()) return;  // stop_ and nothing left to run
-      Job* j = jobs_[next_run_].job.get();
-      lk.unlock();
-      run_(*j);
-      lk.lock();
-      // collect() only pops entries that are done, and this one is not, so
-      // it is still at index next_run_
-      jobs_[next_run_].done = true;
-      ++next_run_;
-      cv_.notify_all();
+      // collect() only pops entries that are done, and none at or past
+      // next_start_ is, so jobs_[next_start_] is the next job to start
+      if (next_start_ < jobs_.size() && (int)flying.size() < depth_) {
+        Job* j = jobs_[next_start_].job.get();
+        ++next_start_;
+        lk.unlock();
+        const bool fly = start_(*j);
+        lk.lock();
+        if (fly) flying.push_back(j);
+        else mark_done(j);
+        continue;
+      }
+      if (!flying.empty()) {
+        Job* j = flying.front();
+        if ((int)flying.size() < depth_ && !stop_) {
+          // a slot is free but nothing to start: finish the oldest once its
+          // device work is done, and start a job that arrives meanwhile first
+          lk.unlock();
+          const bool rdy = ready_(*j);
+          lk.lock();
+          if (!rdy) {
+            // (system_clock: pthread_cond_timedwait, which ThreadSanitizer
+            // intercepts; a steady_clock wait maps to pthread_cond_clockwait)
+            cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::microseconds(kPollUs),
+                           [this] { return stop_ || next_start_ < jobs_.size(); });
+            continue;
+          }
+        }
+        flying.pop_front();
+        lk.unlock();
+        finish_(*j);
+        lk.lock();
+        mark_done(j);
+        continue;
+      }
+      if (stop_ && next_start_ >= jobs_.size()) return;  // nothing queued or in flight
+      cv_.wait(lk, [this] { return stop_ || next_start_ < jobs_.size(); });
     }
   }
 
-  Runner run_;
+  Start start_;
+  Ready ready_;
+  Finish finish_;
+  int depth_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Entry> jobs_;  // submitted and not yet collected, oldest first
-  size_t next_run_ = 0;     // jobs_[next_run_..] have not run
+  size_t next_start_ = 0;   // jobs_[next_start_..] have not started
   bool stop_ = false;
   std::thread worker_;
 };

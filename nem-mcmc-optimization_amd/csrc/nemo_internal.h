@@ -122,24 +122,30 @@ struct Ctx {
   // pinned host staging of the host-pointer entry points (hipHostMalloc):
   // pageable hipMemcpyAsync blocks the host ~0.1 ms per 512 KB, a memcpy into
   // pinned memory plus a DMA copy costs a fraction of that
-  void* h_stage = nullptr;
-  size_t h_stage_bytes = 0;
+  // slot 0: the synchronous nemo_optimal_weights; slots 1 and 2: the queued
+  // calls (nemo_optimal_weights_begin), two in flight so the library thread
+  // stages the next call while the device runs the previous one
+  static constexpr int kStepSlots = 3;
+  void* h_stage[kStepSlots] = {};
+  size_t h_stage_bytes[kStepSlots] = {};
   // device mirror of the staging layout of nemo_optimal_weights (one copy each way)
-  void* d_step = nullptr;
-  size_t d_step_bytes = 0;
+  void* d_step[kStepSlots] = {};
+  size_t d_step_bytes[kStepSlots] = {};
+  hipEvent_t step_done[kStepSlots] = {};  // recorded after a slot's D2H copy
 
   // hipGraphs of nemo_optimal_weights' device work (one H2D copy, the
   // launches, one D2H copy) per (nchains, cap, sig0, sig1); graph_epoch moves
   // whenever a captured argument may change (buffers, options, staging)
   struct StepGraph {
-    int nchains = -1, cap = -1;
+    int nchains = -1, cap = -1, slot = -1;
     double sig0 = 0.0, sig1 = 0.0;
     uint64_t epoch = 0;
     hipGraphExec_t exec = nullptr;
   };
   int graphs = 1;                  // option "graphs": replay the fused step as a hipGraph
   uint64_t graph_epoch = 1;
-  StepGraph step_graph[4];
+  static constexpr int kStepGraphs = 8;
+  StepGraph step_graph[kStepGraphs];
   int step_graph_next = 0;
 
   // timing of the score kernel

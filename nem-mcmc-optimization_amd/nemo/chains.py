@@ -190,7 +190,7 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     chains' states are unspecified afterwards (see the pipeline below).
     ``pool`` (an ``InvPool``) runs the ancestor_x inversions in worker
     processes; the results do not change.  ``groups``: the number of chain
-    groups in the pipeline below (default 3 from 48 chains, else 2)."""
+    groups in the pipeline below (default 3 from 6 chains, else 2)."""
     n = len(chains)
     s = chains[0].num_s
     if state is None:
@@ -254,7 +254,7 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     # next order: with raise_on_fail the exception leaves the chains' states
     # (orders, weights, RNG streams) unspecified -- only the results of runs
     # that complete are defined to equal a sequential batched run.
-    n_groups = 1 if (use_nem or n < 2) else (groups or (3 if n >= 48 else 2))
+    n_groups = 1 if (use_nem or n < 2) else (groups or (3 if n >= 6 else 2))
     n_groups = max(1, min(n_groups, n))
     bounds = [n * g // n_groups for g in range(n_groups + 1)]
     glist = [list(range(bounds[g], bounds[g + 1])) for g in range(n_groups)]

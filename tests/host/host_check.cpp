@@ -238,6 +238,92 @@ struct Job {
   int rc = 0;
 };
 
+// the pipelined form (nemo_optimal_weights_begin): start() puts a job "on the
+// device" (a deadline) unless it fails at once, ready() polls the deadline,
+// finish() waits for it and writes the output.  At most `depth` jobs in
+// flight, started in submission order, finished in the same order, each
+// collected after its finish; shutdown still drains everything
+struct PJob {
+  int id;
+  double* out;
+  int rc = 0;
+  std::chrono::steady_clock::time_point due{};
+  bool started = false, finished = false;
+};
+
+static void check_pipelined_queue(std::mt19937_64& rng) {
+  using clk = std::chrono::steady_clock;
+  for (int depth : {1, 2, 3}) {
+    std::atomic<int> in_flight{0}, max_flight{0}, last_started{-1}, last_finished{-1};
+    std::atomic<bool> order_ok{true};
+    std::mutex rmu;
+    std::mt19937_64 jr(rng());
+    auto start = [&](PJob& j) {
+      if (j.id != last_started + 1) order_ok = false;
+      last_started = j.id;
+      j.started = true;
+      if (j.id % 7 == 6) {  // fails at start: complete at once, never in flight
+        j.rc = -3;
+        *j.out = -3.0;
+        return false;
+      }
+      unsigned us;
+      {
+        std::lock_guard<std::mutex> g(rmu);
+        us = (unsigned)(jr() % 120);
+      }
+      j.due = clk::now() + std::chrono::microseconds(us);
+      const int f = ++in_flight;
+      int m = max_flight.load();
+      while (f > m && !max_flight.compare_exchange_weak(m, f)) {
+      }
+      return true;
+    };
+    auto ready = [](PJob& j) { return clk::now() >= j.due; };
+    auto finish = [&](PJob& j) {
+      std::this_thread::sleep_until(j.due);
+      if (j.id <= last_finished) order_ok = false;
+      last_finished = j.id;
+      *j.out = 10.0 * j.id;
+      j.finished = true;
+      --in_flight;
+    };
+    {
+      StepQueue<PJob> q(start, ready, finish, depth);
+      std::vector<double> out(300, -1.0);
+      std::vector<std::unique_ptr<PJob>> back;
+      int next = 0, got = 0;
+      while (got < 300) {
+        const int burst = 1 + (int)(rng() % 4);
+        for (int k = 0; k < burst && next < 300; ++k, ++next)
+          CHECK(q.submit(std::unique_ptr<PJob>(new PJob{next, &out[next]}), nullptr));
+        if (rng() % 3 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 200));
+        const int take = (int)(rng() % 3);
+        for (int k = 0; k < take && got < next; ++k, ++got) {
+          std::unique_ptr<PJob> j = q.collect();
+          const bool failed = got % 7 == 6;
+          CHECK(j && j->id == got && j->started && j->finished == !failed);
+          CHECK(out[got] == (failed ? -3.0 : 10.0 * got) && j->rc == (failed ? -3 : 0));
+        }
+      }
+      CHECK(q.collect() == nullptr && q.pending() == 0);
+    }
+    CHECK(order_ok.load() && max_flight.load() <= depth && in_flight.load() == 0);
+    // shutdown with jobs queued and in flight: all of them finish
+    {
+      std::vector<double> out(40, -1.0);
+      last_started = -1;
+      last_finished = -1;
+      StepQueue<PJob> q(start, ready, finish, depth);
+      const int n = 1 + (int)(rng() % 40);
+      for (int k = 0; k < n; ++k) CHECK(q.submit(std::unique_ptr<PJob>(new PJob{k, &out[k]}), nullptr));
+      q.shutdown();
+      for (int k = 0; k < n; ++k) CHECK(out[k] == (k % 7 == 6 ? -3.0 : 10.0 * k));
+      CHECK(in_flight.load() == 0);
+    }
+  }
+}
+
 static void check_step_queue(std::mt19937_64& rng) {
   // collected in submission order, each after it ran
   {
@@ -284,6 +370,7 @@ static void check_step_queue(std::mt19937_64& rng) {
   }
   // a queue destroyed without shutdown or any job
   { StepQueue<Job> q([](Job&) {}); }
+  check_pipelined_queue(rng);
 }
 
 int main() {
