@@ -627,8 +627,10 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
 
 // every transfer of a fused step goes through a pinned staging slot: [pos |
 // w01 | anc | w_new | info | ll1 | ll_dag], each part 256-B aligned, and a
-// device block with the same layout: one H2D of [pos .. info] (info preset to
-// -1 = not a permissible pair) and one D2H of [w_new .. ll_dag]
+// device block with the same layout: one H2D of [pos .. anc], info preset to
+// -1 (= not a permissible pair) on the device, one D2H of [w_new .. ll_dag];
+// the host hands back w_new at the entries info marks (the caller's values
+// stay everywhere else)
 struct StepLayout {
   size_t o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, total;
   StepLayout(size_t S, size_t n) {
@@ -665,13 +667,12 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   memcpy(hs, pos, n * S * 4);
   memcpy(hs + L.o_w01, w01, n * S * S * 8);
   memcpy(hs + L.o_anc, anc, n * S * S * 8);
-  memcpy(hs + L.o_wn, w_new, n * S * S * 8);  // entries outside the permissible pairs keep the caller's values
-  memset(hs + L.o_inf, 0xff, n * S * S * 4);
   // replayed as a hipGraph per (nchains, cap, slot) while no captured
   // argument changes (the staging buffers, options and tables bump
   // graph_epoch), so a step costs one graph launch instead of ~10 API calls
   auto enqueue = [&]() -> int {
-    HIPCHK(hipMemcpyAsync(ds, hs, L.o_ll1, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ds, hs, L.o_wn, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(ds + L.o_inf, 0xff, n * S * S * 4, st));
     int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
                                      (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
                                      (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st);
@@ -736,21 +737,26 @@ static int step_finish(nemo_ctx* ctx, int slot, int nchains, double* w_new, doub
   const StepLayout L(S, n);
   HIPCHK(hipEventSynchronize(c.step_done[slot]));
   const char* hs = (const char*)c.h_stage[slot];
-  memcpy(w_new, hs + L.o_wn, n * S * S * 8);
   memcpy(ll1, hs + L.o_ll1, n * 8);
   memcpy(ll_dag, hs + L.o_lld, n * 8);
   if (info) memcpy(info, hs + L.o_inf, n * S * S * 4);
   const int32_t* inf = (const int32_t*)(hs + L.o_inf);
-  for (size_t k = 0; k < n * S * S; ++k) {
-    if (inf[k] == -1) continue;  // not a permissible pair
-    const int status = inf[k] & 15;
-    if (status >= NEMO_LBFGSB_ABNORMAL) {
-      const size_t b = k / (S * S), i = (k / S) % S, j = k % S;
-      return fail(NEMO_ERR_OPT, "Minimization not successful, Reason: %s (chain %zu, pair %zu<-%zu)",
-                  status == NEMO_LBFGSB_ABNORMAL ? "ABNORMAL_TERMINATION_IN_LNSRCH"
-                                                 : "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT",
-                  b, i, j);
+  const double* wn = (const double*)(hs + L.o_wn);
+  const size_t nn = n * S * S;
+  // branch-free blend (vectorised): the caller's value stays where info is -1
+  for (size_t k = 0; k < nn; ++k) w_new[k] = inf[k] != -1 ? wn[k] : w_new[k];
+  size_t bad = SIZE_MAX;  // first failed pair in index order
+  for (size_t k = 0; k < nn; ++k)
+    if (inf[k] != -1 && (inf[k] & 15) >= NEMO_LBFGSB_ABNORMAL) {
+      bad = k;
+      break;
     }
+  if (bad != SIZE_MAX) {
+    const size_t b = bad / (S * S), i = (bad / S) % S, j = bad % S;
+    return fail(NEMO_ERR_OPT, "Minimization not successful, Reason: %s (chain %zu, pair %zu<-%zu)",
+                (inf[bad] & 15) == NEMO_LBFGSB_ABNORMAL ? "ABNORMAL_TERMINATION_IN_LNSRCH"
+                                                       : "STOP: TOTAL NO. of ITERATIONS REACHED LIMIT",
+                b, i, j);
   }
   return NEMO_OK;
 }
