@@ -126,9 +126,12 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* c, const double* anc, con
  * (sigma(x*) > 0.5 ? sig1 : sig0, sig0 = expit(0), sig1 = expit(1)).
  *   anc    [nchains][S][S]  clip(inv(I - expit_parent_weights(W)) - I, 0, 1)
  *   w_new  [nchains][S][S]  expit(x*) at permissible entries (others untouched)
- *   info   [nchains][S][S]  nullable; status | nit << 4 | nfev << 16 per pair
+ *   info   [nchains][S][S]  nullable; status | nit << 4 | nfev << 16 per pair,
+ *                           -1 at entries that are not a permissible pair
  *   ll1, ll_dag [nchains]
- * Returns NEMO_ERR_OPT (results still written) if any pair ended abnormally. */
+ * Returns NEMO_ERR_OPT (results still written) if any pair ended abnormally.
+ * _dev: the same on device pointers, queued on `stream` (null: the context's),
+ * without the NEMO_ERR_OPT check (read it from d_info). */
 int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
                          const double* anc, double sig0, double sig1, int cap, double* w_new,
                          double* ll1, double* ll_dag, int32_t* info);

@@ -605,15 +605,24 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
     return fail(NEMO_ERR_ARG, "null device pointer");
   hipStream_t st = pick(ctx, stream);
   const int npairs = nemo::pairs_per_chain(c.S, cap);
-  // eval #1 with order weights (nem_order_mcmc.py:181-182)
-  HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, c.d_pairs, st));
-  if (use_factored(c))
-    HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, d_w01, d_ll1, nullptr, nullptr, c.d_ow, st));
-  else
+  // eval #1 with order weights (nem_order_mcmc.py:181-182).  Factored: one
+  // prep launch for the pair lists (info rows preset to -1) and eval #1's
+  // Delta, and eval #1's partial sums ride in the local-optimum launch -- two
+  // launches fewer per step (a graph node costs ~5 us however small its kernel)
+  nemo::FinalizeArgs fin;
+  if (use_factored(c)) {
+    HIPCHK(nemo::launch_step_prep(c, nchains, cap, d_pos, d_w01, d_info, st));
+    int np = 0;
+    HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, d_w01, d_ll1, nullptr, nullptr, c.d_ow, st,
+                                       true, &np));
+    if (np > 0) fin = nemo::FinalizeArgs{c.d_fpartial, np, nchains, d_ll1};
+  } else {
+    HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, c.d_pairs, st, d_info));
     HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll1, nullptr, nullptr, c.d_ow, st));
+  }
   // every permissible pair's local optimum (nem_order_mcmc.py:186-189)
   HIPCHK(nemo::launch_local_opt_pairs(c, nchains, npairs, c.d_pairs, c.d_rows, d_w01, d_anc, c.d_ow,
-                                      sig0, sig1, d_w_new, c.d_wdag, d_info, st));
+                                      sig0, sig1, d_w_new, c.d_wdag, d_info, st, fin));
   // eval #2 on the binarised weights (nem_order_mcmc.py:205-207)
   if (use_factored(c)) {
     HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, c.d_wdag, d_ll_dag, nullptr, nullptr, nullptr, st));
@@ -628,7 +637,7 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
 // every transfer of a fused step goes through a pinned staging slot: [pos |
 // w01 | anc | w_new | info | ll1 | ll_dag], each part 256-B aligned, and a
 // device block with the same layout: one H2D of [pos .. anc], info preset to
-// -1 (= not a permissible pair) on the device, one D2H of [w_new .. ll_dag];
+// -1 (= not a permissible pair) by the step's prep, one D2H of [w_new .. ll_dag];
 // the host hands back w_new at the entries info marks (the caller's values
 // stay everywhere else)
 struct StepLayout {
@@ -671,8 +680,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   // argument changes (the staging buffers, options and tables bump
   // graph_epoch), so a step costs one graph launch instead of ~10 API calls
   auto enqueue = [&]() -> int {
-    HIPCHK(hipMemcpyAsync(ds, hs, L.o_wn, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(ds + L.o_inf, 0xff, n * S * S * 4, st));
+    HIPCHK(hipMemcpyAsync(ds, hs, L.o_wn, hipMemcpyHostToDevice, st));  // info: preset by the prep
     int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
                                      (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
                                      (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st);

@@ -109,11 +109,46 @@ __device__ __forceinline__ int fxcd_work_index(int L, int N, int remap) {
 // Dp [b][SPAD][SPAD] (row = child position q, col = parent position p),
 // G  [b][SPAD], permo [b][SPAD] (node at position q; S for padding rows).
 // ---------------------------------------------------------------------------
+// one wave: row q (child position q) of Delta and its G, for the order in
+// perm (LDS); padding rows (q >= S) carry zeros and a finite "no row" G
+__device__ __forceinline__ void delta_row(int S, int SPAD, int cap, int b, int q, const int* perm,
+                                          const double* __restrict__ w01, const double* __restrict__ e_lo,
+                                          const double* __restrict__ e_hi, double* __restrict__ Dp,
+                                          double* __restrict__ G, int lane) {
+  const int i = q < S ? perm[q] : 0;
+  const double* wrow = w01 + ((size_t)b * S + i) * S;
+  double* drow = Dp + ((size_t)b * SPAD + q) * SPAD;
+  double gsum = 0.0;
+  for (int p0 = 0; p0 < SPAD; p0 += kWave) {
+    const int p = p0 + lane;
+    double d = 0.0, glo = 0.0;
+    const bool ok = q < S && p < q && (cap == 0 || q - p <= cap);
+    if (ok) {
+      const int j = perm[p];
+      const double s = wrow[j];
+      const double lo = log(fma(s, e_lo[j] - 1.0, 1.0));
+      const double hi = log(fma(s, e_hi[j] - 1.0, 1.0));
+      d = hi - lo;
+      glo = lo;
+    }
+    if (p < SPAD && p != (q | 15)) drow[p] = d;
+    gsum += fwave_sum(glo);
+  }
+  if (lane == 0) {
+    G[(size_t)b * SPAD + q] = gsum;
+    // column 16r+15 of row block r is never a parent of rows 16r..16r+15:
+    // it carries G (the score kernels multiply it by 1), and a finite
+    // "no row" value on padding rows
+    drow[q | 15] = q < S ? gsum : kPadG;
+  }
+}
+
 __global__ __launch_bounds__(256) void prep_factored_kernel(
     int S, int SPAD, int cap, const int32_t* __restrict__ pos, const double* __restrict__ w01,
     const double* __restrict__ e_lo, const double* __restrict__ e_hi, double* __restrict__ Dp,
     double* __restrict__ G, int32_t* __restrict__ permo) {
   __shared__ int perm[kMaxS];
+  __shared__ int scan[kMaxS];
   // block = (evaluation, group of 4 child positions); one row per wave (the
   // rows of one evaluation spread over SPAD / 4 blocks: a lone evaluation's
   // prep is a quarter of the serial work per wave it was with 16-row blocks)
@@ -121,47 +156,35 @@ __global__ __launch_bounds__(256) void prep_factored_kernel(
   const int b = blockIdx.x / ngroups;
   const int grp = blockIdx.x - b * ngroups;
   const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
-  for (int k = tid; k < S; k += blockDim.x) perm[k] = 0;
-  __syncthreads();
-  for (int i = tid; i < S; i += blockDim.x) {
-    int pi = pos[(size_t)b * S + i];
-    pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);  // malformed input must not fault
-    perm[pi] = i;
-  }
-  __syncthreads();
+  prep_order_lds(S, cap, pos + (size_t)b * S, perm, scan, false);
   if (grp == 0)
     for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
-  const int nw = blockDim.x / kWave;
-  for (int q = 4 * grp + w; q < 4 * grp + 4; q += nw) {
-    const int i = q < S ? perm[q] : 0;
-    const double* wrow = w01 + ((size_t)b * S + i) * S;
-    double* drow = Dp + ((size_t)b * SPAD + q) * SPAD;
-    double gsum = 0.0;
-    for (int p0 = 0; p0 < SPAD; p0 += kWave) {
-      const int p = p0 + lane;
-      double d = 0.0, glo = 0.0;
-      const bool ok = q < S && p < q && (cap == 0 || q - p <= cap);
-      if (ok) {
-        const int j = perm[p];
-        const double s = wrow[j];
-        const double lo = log(fma(s, e_lo[j] - 1.0, 1.0));
-        const double hi = log(fma(s, e_hi[j] - 1.0, 1.0));
-        d = hi - lo;
-        glo = lo;
-      }
-      if (p < SPAD && p != (q | 15)) drow[p] = d;
-      gsum += fwave_sum(glo);
-    }
-    if (lane == 0) {
-      G[(size_t)b * SPAD + q] = gsum;
-      // column 16r+15 of row block r is never a parent of rows 16r..16r+15:
-      // it carries G (the score kernels multiply it by 1), and a finite
-      // "no row" value on padding rows
-      drow[q | 15] = q < S ? gsum : kPadG;
-    }
-  }
+  const int q = 4 * grp + tid / kWave;
+  delta_row(S, SPAD, cap, b, q, perm, w01, e_lo, e_hi, Dp, G, tid & (kWave - 1));
+}
+
+// the fused step's prep (nemo_optimal_weights_dev): prep_kernel's work for
+// children 4 g .. 4 g + 3 and prep_factored_kernel's for positions 4 g ..
+// 4 g + 3 in one block g of the evaluation -- the same arithmetic, one
+// launch (a graph node costs ~5 us however small its kernel)
+__global__ __launch_bounds__(256) void step_prep_kernel(
+    int S, int SPAD, int cap, const int32_t* __restrict__ pos, const double* __restrict__ w01,
+    const double* __restrict__ e_lo, const double* __restrict__ e_hi, int32_t* __restrict__ rows,
+    double* __restrict__ sw, int32_t* __restrict__ cnt, int32_t* __restrict__ pairs, int32_t* __restrict__ info,
+    double* __restrict__ Dp, double* __restrict__ G, int32_t* __restrict__ permo) {
+  __shared__ int perm[kMaxS];
+  __shared__ int scan[kMaxS];
+  const int ngroups = max((S + 3) / 4, SPAD / 4);
+  const int b = blockIdx.x / ngroups;
+  const int grp = blockIdx.x - b * ngroups;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1);
+  const int32_t* pb = pos + (size_t)b * S;
+  prep_order_lds(S, cap, pb, perm, scan, true);
+  if (grp == 0)
+    for (int k = tid; k < SPAD; k += blockDim.x) permo[(size_t)b * SPAD + k] = k < S ? perm[k] : S;
+  const int r = 4 * grp + tid / kWave;  // this wave's child and position
+  if (r < S) prep_child_list(S, cap, pb, w01, rows, sw, cnt, pairs, info, b, r, perm, scan, lane);
+  if (r < SPAD) delta_row(S, SPAD, cap, b, r, perm, w01, e_lo, e_hi, Dp, G, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -578,7 +601,7 @@ int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
 
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
-                                 double* d_ow, hipStream_t st) {
+                                 double* d_ow, hipStream_t st, bool prepped, int* defer_np) {
   const int spad = c.fspad;
   if (cap >= c.S - 1) cap = 0;  // every predecessor is within the cap: no cap (same bits)
   const bool ll_only = !d_cs && !d_cells && !d_ow;
@@ -602,7 +625,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   const bool i8 = fk >= 4 && fk <= 6;
   const bool pipe = fk == 2 || fk == 3;
   hipError_t err = hipSuccess;
-  if (!i8 && !i8o && !win && !wide) {  // the int8 and lookup-table kernels derive their inputs themselves
+  if (!i8 && !i8o && !win && !wide && !prepped) {  // the int8 and lookup-table kernels derive their inputs themselves
     prep_factored_kernel<<<batch * (spad / 4), 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo,
                                                              c.d_ehi, c.d_fDp, c.d_fG, c.d_fperm);
     err = hipGetLastError();
@@ -662,8 +685,20 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     c.launches++;
   }
   // per-evaluation partials, summed in a fixed order
-  if (!finalized)
+  if (defer_np) *defer_np = finalized ? 0 : np;
+  else if (!finalized)
     finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
+  return hipGetLastError();
+}
+
+hipError_t launch_step_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            int32_t* d_info, hipStream_t st) {
+  const int spad = c.fspad;
+  if (cap >= c.S - 1) cap = 0;  // as launch_score_factored (same lists: a cap >= S - 1 cuts nothing)
+  const int ngroups = std::max((c.S + 3) / 4, spad / 4);
+  step_prep_kernel<<<batch * ngroups, 256, 0, st>>>(c.S, spad, cap, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_rows,
+                                                    c.d_sw, c.d_cnt, c.d_pairs, d_info, c.d_fDp, c.d_fG,
+                                                    c.d_fperm);
   return hipGetLastError();
 }
 

@@ -168,7 +168,7 @@ hipError_t launch_knockdown_tables(Ctx& c, const uint8_t* d_D, const double* d_c
                                    double B, hipStream_t st);
 hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                        int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
-                       hipStream_t st);
+                       hipStream_t st, int32_t* d_info = nullptr);
 hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* d_sw,
                         const int32_t* d_cnt, double* d_ll, double* d_cs, double* d_cells,
                         double* d_ow, hipStream_t st);
@@ -177,10 +177,19 @@ hipError_t launch_prep_group(Ctx& c, int batch, int group, int cap, const int32_
 hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStream_t st);
 hipError_t launch_lse(Ctx& c, int rows, const double* d_cells, double* d_ll, double* d_cs,
                       double* d_ow, hipStream_t st);
+// fin: when fin_ll is set, the launch also sums the fin_n partials per
+// evaluation of fin_batch evaluations into fin_ll (finalize_factored_kernel's
+// work, in blocks appended to the grid: one launch less in the fused step)
+struct FinalizeArgs {
+  const double* partial = nullptr;
+  int n = 0, batch = 0;
+  double* ll = nullptr;
+};
 hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
                                   const int32_t* d_rows, const double* d_w01, const double* d_anc,
                                   const double* d_ow, double sig0, double sig1, double* d_wnew,
-                                  double* d_wdag, int32_t* d_info, hipStream_t st);
+                                  double* d_wdag, int32_t* d_info, hipStream_t st,
+                                  FinalizeArgs fin = FinalizeArgs{});
 // prod: the objective as one log of a product per lane (every factor 1 + c e,
 // e in (0, 1), within [1e-30, 1e30]; the caller checks)
 hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
@@ -319,6 +328,64 @@ __device__ __forceinline__ void fill_log_table(double2* ltab, int tid, int nthre
   }
 }
 
+// ---- the per-evaluation prep shared by prep_kernel and step_prep_kernel ----
+// the evaluation's order in LDS (block of >= S threads): perm[p] = the node
+// at position p; with want_scan, scan[i] = inclusive prefix sum of the list
+// lengths of children 0..i (Hillis-Steele).  Malformed positions are clamped
+// (they must not fault; the host rejects them first).
+__device__ __forceinline__ void prep_order_lds(int S, int cap, const int32_t* __restrict__ pb, int* perm,
+                                               int* scan, bool want_scan) {
+  const int tid = threadIdx.x;
+  if (tid < S) perm[tid] = 0;
+  __syncthreads();
+  if (tid < S) {
+    int p = pb[tid];
+    p = p < 0 ? 0 : (p >= S ? S - 1 : p);
+    perm[p] = tid;
+    const int lo = (cap > 0 && p > cap) ? p - cap : 0;
+    scan[tid] = p - lo;  // list length of child tid
+  }
+  __syncthreads();
+  if (want_scan) {
+    for (int o = 1; o < S; o <<= 1) {
+      const int v = (tid < S && tid >= o) ? scan[tid - o] : 0;
+      __syncthreads();
+      if (tid < S) scan[tid] += v;
+      __syncthreads();
+    }
+  }
+}
+
+// one wave: child i's permissible parents in pi order (nem_order_mcmc.py:
+// 62-65; with cap, the last `cap` of them), their weights, the list length,
+// the child's slots of the flat pair list (when pairs), and -1 in every entry
+// of its info row (when info: "not a permissible pair"; the local optima
+// overwrite theirs)
+__device__ __forceinline__ void prep_child_list(int S, int cap, const int32_t* __restrict__ pb,
+                                                const double* __restrict__ w01, int32_t* __restrict__ rows,
+                                                double* __restrict__ sw, int32_t* __restrict__ cnt,
+                                                int32_t* __restrict__ pairs, int32_t* __restrict__ info, int b,
+                                                int i, const int* perm, const int* scan, int lane) {
+  int pi = pb[i];
+  pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);
+  const int lo = (cap > 0 && pi > cap) ? pi - cap : 0;
+  const int n = pi - lo;
+  const size_t row = ((size_t)b * S + i) * S;
+  int32_t* r = rows + row;
+  double* w = sw + row;
+  const double* wr = w01 + row;
+  int32_t* pr = pairs ? pairs + (size_t)b * S * S + (scan[i] - n) : nullptr;
+  if (info)
+    for (int t = lane; t < S; t += kWave) info[row + t] = -1;
+  for (int t = lane; t < n; t += kWave) {
+    const int j = perm[lo + t];
+    r[t] = j;
+    w[t] = wr[j];
+    if (pr) pr[t] = (i << 16) | t;
+  }
+  if (lane == 0) cnt[(size_t)b * S + i] = n;
+}
+
 // fixed-order sum of n partials by one wave: strided lane sums, then an xor
 // tree (finalize_factored_kernel and the int8 kernel's own finalize share it,
 // so both paths give identical bits)
@@ -339,9 +406,17 @@ hipError_t launch_ancestral(Ctx& c, int nprob, const int32_t* d_pos, const doubl
 // then the commit of the level's optima into d_w
 hipError_t launch_inverse_level(Ctx& c, int n, const int32_t* d_list, const int32_t* d_pos, double* d_w,
                                 const double* d_ow, double* d_xout, int32_t* d_info, hipStream_t st);
+// prepped: Delta / G / perm of the batch are already staged (step_prep_kernel);
+// defer_np: when set, the per-evaluation partials are left unsummed and
+// *defer_np = their count (0 if the kernel summed them itself)
 hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_pos,
                                  const double* d_w01, double* d_ll, double* d_cs, double* d_cells,
-                                 double* d_ow, hipStream_t st);
+                                 double* d_ow, hipStream_t st, bool prepped = false,
+                                 int* defer_np = nullptr);
+// the fused step's prep in ONE launch: prep_kernel's parent and pair lists
+// with the info rows preset to -1, and prep_factored_kernel's Delta / G / perm
+hipError_t launch_step_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
+                            int32_t* d_info, hipStream_t st);
 // the fact_kernel value a factored call takes (the option, or what auto
 // resolves to for this cap / output set), with the worst-case |ll error| of
 // its fixed-point arithmetic (0 for the fp64 kernels); -1 if none applies

@@ -98,48 +98,16 @@ __global__ void exp_table_kernel(size_t n, const double* __restrict__ t64, TT* _
 __global__ __launch_bounds__(256) void prep_kernel(int S, int cap, const int32_t* __restrict__ pos,
                                                    const double* __restrict__ w01, int32_t* __restrict__ rows,
                                                    double* __restrict__ sw, int32_t* __restrict__ cnt,
-                                                   int32_t* __restrict__ pairs) {
+                                                   int32_t* __restrict__ pairs, int32_t* __restrict__ info) {
   __shared__ int perm[kMaxS];
   __shared__ int scan[kMaxS];
   const int nblk = (S + 3) / 4;
   const int b = blockIdx.x / nblk;
   const int i = (blockIdx.x - b * nblk) * 4 + (int)(threadIdx.x / kWave);  // this wave's child
-  const int tid = threadIdx.x, lane = tid & (kWave - 1);
   const int32_t* pb = pos + (size_t)b * S;
-  if (tid < S) perm[tid] = 0;
-  __syncthreads();
-  if (tid < S) {
-    int p = pb[tid];
-    p = p < 0 ? 0 : (p >= S ? S - 1 : p);  // malformed input must not fault
-    perm[p] = tid;
-    const int lo = (cap > 0 && p > cap) ? p - cap : 0;
-    scan[tid] = p - lo;  // list length of child tid
-  }
-  __syncthreads();
-  if (pairs != nullptr) {  // inclusive prefix sums of the lengths (Hillis-Steele)
-    for (int o = 1; o < S; o <<= 1) {
-      const int v = (tid < S && tid >= o) ? scan[tid - o] : 0;
-      __syncthreads();
-      if (tid < S) scan[tid] += v;
-      __syncthreads();
-    }
-  }
+  prep_order_lds(S, cap, pb, perm, scan, pairs != nullptr);
   if (i >= S) return;  // uniform per wave
-  int pi = pb[i];
-  pi = pi < 0 ? 0 : (pi >= S ? S - 1 : pi);
-  const int lo = (cap > 0 && pi > cap) ? pi - cap : 0;
-  const int n = pi - lo;
-  int32_t* r = rows + ((size_t)b * S + i) * S;
-  double* w = sw + ((size_t)b * S + i) * S;
-  const double* wr = w01 + ((size_t)b * S + i) * S;
-  int32_t* pr = pairs ? pairs + (size_t)b * S * S + (scan[i] - n) : nullptr;
-  for (int t = lane; t < n; t += kWave) {
-    const int j = perm[lo + t];
-    r[t] = j;
-    w[t] = wr[j];
-    if (pr) pr[t] = (i << 16) | t;
-  }
-  if (lane == 0) cnt[(size_t)b * S + i] = n;
+  prep_child_list(S, cap, pb, w01, rows, sw, cnt, pairs, info, b, i, perm, scan, threadIdx.x & (kWave - 1));
 }
 
 // ---------------------------------------------------------------------------
@@ -516,14 +484,34 @@ constexpr int kLocalOptWavesPerSimd = NEMO_LOCAL_OPT_WAVES;
 #endif
 constexpr int kLocalSplitMax = NEMO_LOCAL_SPLIT_MAX;
 
-// pairs of the fused per-step scorer.  grid covers nchains * npairs waves.
+// eval #1's partial sums alone (the split local-optimum path and steps with
+// no pair): finalize_factored_kernel's work
+__global__ void finalize_factored_sums(FinalizeArgs fin) {
+  const int e = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
+  const int lane = threadIdx.x & (kWave - 1);
+  if (e >= fin.batch) return;
+  const double v = sum_partials(fin.partial + (size_t)e * fin.n, fin.n, lane);
+  if (lane == 0) fin.ll[e] = v;
+}
+
+// pairs of the fused per-step scorer.  grid covers nchains * npairs waves
+// (lo_blocks blocks of 4), then the appended finalize blocks of `fin`.
 template <typename TT, int NPL, bool PROD>
 __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_kernel(
     int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
     const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
     const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
     double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
-    int32_t* __restrict__ info) {
+    int32_t* __restrict__ info, int lo_blocks, FinalizeArgs fin) {
+  if ((int)blockIdx.x >= lo_blocks) {  // appended blocks: eval #1's partial sums, one wave per evaluation
+    const int e = ((int)blockIdx.x - lo_blocks) * 4 + (int)(threadIdx.x / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (e < fin.batch) {
+      const double v = sum_partials(fin.partial + (size_t)e * fin.n, fin.n, lane);
+      if (lane == 0) fin.ll[e] = v;
+    }
+    return;
+  }
   __shared__ double2 ltab[128];
   fill_log_table(ltab, threadIdx.x, blockDim.x);
   __syncthreads();
@@ -752,8 +740,9 @@ hipError_t launch_exp_table(Ctx& c, const double* d_T64, hipStream_t st) {
 
 hipError_t launch_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                        int32_t* d_rows, double* d_sw, int32_t* d_cnt, int32_t* d_pairs,
-                       hipStream_t st) {
-  prep_kernel<<<batch * ((c.S + 3) / 4), 256, 0, st>>>(c.S, cap, d_pos, d_w01, d_rows, d_sw, d_cnt, d_pairs);
+                       hipStream_t st, int32_t* d_info) {
+  prep_kernel<<<batch * ((c.S + 3) / 4), 256, 0, st>>>(c.S, cap, d_pos, d_w01, d_rows, d_sw, d_cnt, d_pairs,
+                                                        d_info);
   return hipGetLastError();
 }
 
@@ -872,9 +861,10 @@ template <typename TT>
 static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
                                 const int32_t* d_rows, const double* d_w01, const double* d_anc,
                                 const double* d_ow, double sig0, double sig1, double* d_wnew,
-                                double* d_wdag, int32_t* d_info, hipStream_t st) {
+                                double* d_wdag, int32_t* d_info, hipStream_t st, FinalizeArgs fin) {
   const size_t waves = (size_t)nchains * npairs;
-  const int blocks = (int)((waves + 3) / 4);
+  const int lo_blocks = (int)((waves + 3) / 4);
+  const int blocks = lo_blocks + (fin.ll ? (fin.batch + 3) / 4 : 0);
   const TT* eT = (const TT*)c.d_eT;
   // the product form needs every 4 factors in range (LocalObjective)
   const bool prod = c.local_prod && c.table_absmax <= 40.0;
@@ -884,6 +874,8 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
   const bool splittable = prod && (npl == 16 || npl == 32 || npl == 64);
   const bool split = splittable && (c.local_split == 2 || (c.local_split == 0 && waves <= (size_t)kLocalSplitMax));
   if (split) {
+    if (fin.ll)
+      finalize_factored_sums<<<(fin.batch + 3) / 4, 256, 0, st>>>(fin);
     const int nb = (int)waves;
     if (npl == 16)
       local_opt_pairs_split_kernel<TT, 16><<<nb, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
@@ -899,10 +891,10 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
 #define NEMO_LP(NPL)                                                                            \
   if (prod)                                                                                     \
     local_opt_pairs_kernel<TT, NPL, true><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, \
-        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);              \
+        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info, lo_blocks, fin); \
   else                                                                                          \
     local_opt_pairs_kernel<TT, NPL, false><<<blocks, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, \
-        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info)
+        d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info, lo_blocks, fin)
   switch (npl_for(c.E)) {
     case 4: NEMO_LP(4); break;
     case 8: NEMO_LP(8); break;
@@ -920,13 +912,16 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
 hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t* d_pairs,
                                   const int32_t* d_rows, const double* d_w01, const double* d_anc,
                                   const double* d_ow, double sig0, double sig1, double* d_wnew,
-                                  double* d_wdag, int32_t* d_info, hipStream_t st) {
-  if (nchains * npairs == 0) return hipSuccess;
+                                  double* d_wdag, int32_t* d_info, hipStream_t st, FinalizeArgs fin) {
+  if (nchains * npairs == 0) {
+    if (fin.ll) finalize_factored_sums<<<(fin.batch + 3) / 4, 256, 0, st>>>(fin);
+    return hipGetLastError();
+  }
   if (c.dtype == 0)
     return local_pairs_t<double>(c, nchains, npairs, d_pairs, d_rows, d_w01, d_anc, d_ow, sig0,
-                                 sig1, d_wnew, d_wdag, d_info, st);
+                                 sig1, d_wnew, d_wdag, d_info, st, fin);
   return local_pairs_t<float>(c, nchains, npairs, d_pairs, d_rows, d_w01, d_anc, d_ow, sig0, sig1,
-                              d_wnew, d_wdag, d_info, st);
+                              d_wnew, d_wdag, d_info, st, fin);
 }
 
 hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
