@@ -306,6 +306,26 @@ def test_chain_batch_equals_single_chains():
     assert np.array_equal(cbp.accepted, cb.accepted)
 
 
+def test_pipelined_chain_groups_equal_one_batch():
+    """48 chains in three pipelined groups of 16: each group's fused step is
+    queued on the library thread (two steps in flight, staging slots 1 and 2);
+    the trajectories equal one synchronous batch of all 48."""
+    from nemo.chains import ChainBatch
+    m = generator.synthetic_nem(16, 500, 3)
+    nc = 48
+    orders = [np.random.default_rng(100 + k).permutation(16) for k in range(nc)]
+    seeds = [500 + k for k in range(nc)]
+    one = ChainBatch(m, orders, seeds, swap_prob=0.9, groups=1, on_fail="continue")
+    b1, o1 = one.run(6)
+    grp = ChainBatch(m, orders, seeds, swap_prob=0.9, groups=3, engine=one.engine, on_fail="continue")
+    b3, o3 = grp.run(6)
+    assert np.array_equal(b1, b3) and np.array_equal(o1, o3)
+    assert np.array_equal(one.accepted, grp.accepted)
+    for c1, c3 in zip(one.chains, grp.chains):
+        assert np.array_equal(c1.parent_weights, c3.parent_weights)
+        assert c1.all_score_list == c3.all_score_list
+
+
 @pytest.mark.parametrize("name,s,e,cap", [("net2", 11, 184, 0), ("C2", 16, 500, 0), ("C3", 64, 2000, 0),
                                           ("C5cap", 128, 5000, 6)])
 def test_factored_mfma_path_vs_golden_and_stream(name, s, e, cap):
