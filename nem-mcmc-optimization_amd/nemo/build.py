@@ -57,6 +57,48 @@ def build_id(defines=()) -> str:
 
 _FLAGS = ("-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function")
 
+# the translation unit each profiled kernel is compiled in (its device code
+# is that file and what it includes, nothing else)
+KERNEL_TU = {"i8l": "nemo_factored_i8.hip", "i8o": "nemo_factored_i8.hip", "i8s": "nemo_factored_i8.hip",
+             "i8": "nemo_factored_i8.hip", "i8w": "nemo_factored_i8.hip", "factored": "nemo_factored.hip",
+             "stream": "nemo_kernels.hip", "win": "nemo_window.hip", "win2": "nemo_window.hip"}
+
+
+def _include_closure(src: str) -> list:
+    """``src`` and every quoted #include it reaches in csrc/ or include/."""
+    seen, todo = [], [src]
+    while todo:
+        p = todo.pop()
+        if p in seen:
+            continue
+        seen.append(p)
+        with open(p, encoding="utf-8", errors="replace") as fh:
+            for line in fh:
+                s = line.strip()
+                if s.startswith("#include \""):
+                    name = s.split('"')[1]
+                    for d in (SRC_DIR, INCLUDE):
+                        q = os.path.join(d, name)
+                        if os.path.exists(q):
+                            todo.append(q)
+                            break
+    return sorted(seen)
+
+
+def code_id(tu: str, defines=()) -> str:
+    """Hash of ONE translation unit's code (the source, its include closure,
+    the flags and the target).  A profiler record of a kernel names the code
+    id of the unit the kernel is compiled in: a change elsewhere in the
+    library (the C ABI, another kernel file) leaves the kernel's machine code,
+    and so its counters, unchanged."""
+    h = hashlib.sha256()
+    for p in _include_closure(os.path.join(SRC_DIR, tu)):
+        h.update(os.path.relpath(p, REPO).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(repr((ARCH, list(defines), _FLAGS)).encode())
+    return h.hexdigest()[:16]
+
 
 def up_to_date() -> bool:
     if not os.path.exists(LIB):

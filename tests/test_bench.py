@@ -34,6 +34,26 @@ def test_profile_records_are_tied_to_the_build(tmp_path, monkeypatch):
     assert bench.load_record("valu.json", "C3:i8l:b2048", "aaaa") is None
 
 
+def test_profile_record_holds_while_its_kernel_unit_is_unchanged(tmp_path, monkeypatch):
+    # a record of another library build still holds when it names the code id
+    # of the kernel's own translation unit as the tree has it now, and the
+    # loaded library is this tree's build; a changed unit drops it
+    import json
+    sys.path.insert(0, os.path.join(HERE, "nem-mcmc-optimization_amd"))
+    from nemo import build as nb
+    (tmp_path / "profiles").mkdir()
+    cid = nb.code_id(nb.KERNEL_TU["i8l"])
+    assert cid == nb.code_id("nemo_factored_i8.hip") and cid != nb.code_id("nemo_kernels.hip")
+    rec = {"C3:i8l:b2048": {"build_id": "old", "code_id": cid, "bytes_per_launch": 6.66e7},
+           "C3:i8w:b2048": {"build_id": "old", "code_id": "feedfeedfeedfeed", "bytes_per_launch": 1.0}}
+    (tmp_path / "profiles" / "traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    tree = nb.build_id()
+    assert bench.load_record("traffic.json", "C3:i8l:b2048", tree)["bytes_per_launch"] == 6.66e7
+    assert bench.load_record("traffic.json", "C3:i8l:b2048", "a-library-of-another-tree") is None
+    assert bench.load_record("traffic.json", "C3:i8w:b2048", tree) is None
+
+
 def test_roofline_is_a_hardware_fraction(monkeypatch):
     # with the PMC record of the build: bound = VALU issue, frac <= 1 against
     # the max-clock issue peak, the int8 matrix cores and HBM beside it <= 1

@@ -12,7 +12,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
-from nemo.build import build_id  # noqa: E402  (the record names the build it measured)
+from nemo.build import KERNEL_TU, build_id, code_id  # noqa: E402  (the record names the build it measured)
 
 
 def per_kernel(path, counter):
@@ -48,6 +48,8 @@ def main():
                      "fetch_size_kib": f[kind], "write_size_kib": w.get(kind, 0.0),
                      "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE, KiB",
                      "build_id": build_id()}
+        if kind in KERNEL_TU:  # the kernel's own unit: the record holds while it is unchanged
+            data[key]["code_id"] = code_id(KERNEL_TU[kind])
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data, indent=1))
 

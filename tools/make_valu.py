@@ -16,7 +16,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
-from nemo.build import build_id  # noqa: E402  (the record names the build it measured)
+from nemo.build import KERNEL_TU, build_id, code_id  # noqa: E402  (the record names the build it measured)
 
 TAGS = (("score_window2_kernel", "win2"), ("score_window_kernel", "win"), ("score_i8w_kernel", "i8w"), ("score_i8l_kernel", "i8l"), ("score_i8s_kernel", "i8s"), ("score_i8o_kernel", "i8o"), ("score_i8_kernel", "i8"), ("score_factored_pipe_kernel", "pipe"),
         ("score_factored_kernel", "factored"), ("score_kernel", "stream"))
@@ -66,6 +66,8 @@ def main():
                           "SQ_VALU_MFMA_COEXEC_CYCLES / SQ_VALU_MFMA_BUSY_CYCLES (MFMA cycles with a VALU "
                           "issue beside them); lds_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE / 8)")
         rec["build_id"] = build_id()
+        if kind in KERNEL_TU:  # the kernel's own unit: the record holds while it is unchanged
+            rec["code_id"] = code_id(KERNEL_TU[kind])
         data[key] = rec
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data, indent=1))
