@@ -213,7 +213,10 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                18 = the log2 kernel for 64 < S <= 128 (two K = 64 halves,
  *                two tiles per iteration), which auto takes for uncapped
  *                ll-only calls there within the error budget; 19 = the same
- *                with one tile per iteration
+ *                with one tile per iteration; 20 = 10 as two launches, a
+ *                prep-only one writing each evaluation's digits to HBM and a
+ *                walk-only one reading them (10's bits; an experiment,
+ *                measured slower)
  *   "factored"   (get only) 1 if the staged table is factorable
  *   "win"        (get only) 1 if the capped lookup-table kernel is staged
  *                (U - U[S] two-valued per row, partial sums in range)

@@ -143,7 +143,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -183,6 +183,7 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_fperm, nb * sp));
     HIPCHK(dalloc(&c.d_fpartial, nb * (size_t)nemo::factored_partials(c)));
     c.cap_batch = nb;
+    if (c.fact_kernel == 20) HIPCHK(nemo::i8img_reserve(c));
   }
   const int nc = std::max(max_chains, 1);
   if (nc > c.cap_chains) {
@@ -991,8 +992,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "fact_kernel") == 0) {
-    if (value < 0 || value > 19) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..19", value);
+    if (value < 0 || value > 20) return fail(NEMO_ERR_ARG, "fact_kernel=%d not in 0..20", value);
     ctx->c.fact_kernel = value;
+    if (value == 20) return nemo::i8img_reserve(ctx->c) == hipSuccess ? NEMO_OK
+                                                                      : fail(NEMO_ERR_HIP, "fact_kernel 20: image buffer");
     return NEMO_OK;
   }
   if (strcmp(name, "local_prod") == 0) {

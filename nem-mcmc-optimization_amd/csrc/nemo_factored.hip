@@ -614,7 +614,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // SIMD; 10 walks two effect tiles per iteration, 16 is the same kernel with
   // one; 17: 10's walk in persistent blocks that prep the next evaluation
   // during the walk; 18 / 19 the log2 kernel for 64 < S <= 128 with two / one
-  // tiles per iteration)
+  // tiles per iteration; 20: 10 as a prep-only and a walk-only launch)
   const int fk = resolve_fact_kernel(c, cap, ll_only, nullptr);
   if (fk < 0) return hipErrorInvalidValue;  // asked for a kernel the staged model does not support
   const bool is_auto = c.fact_kernel == 0;
@@ -647,7 +647,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     // 7 / 8: offset log-sum-exp with 4 / 8 waves per block; 10 (auto's l2
     // choice): 8 waves, two effect tiles per iteration; 11: 4 waves; 12: 16;
     // 16: 8 waves, one tile per iteration
-    const int waves = fk == 17 ? -3 : fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : fk == 12 ? 16
+    const int waves = fk == 20 ? -20 : fk == 17 ? -3 : fk == 13 ? 0 : fk == 14 ? -8 : fk == 16 ? 8 : fk == 12 ? 16
                     : (fk == 7 || fk == 11) ? 4 : fk == 10 ? -2 : 8;
     err = launch_score_i8o(c, batch, cap, d_pos, d_w01, d_ll, waves, l2, st, &np, &finalized);
   } else if (i8) {

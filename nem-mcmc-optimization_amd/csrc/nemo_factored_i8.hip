@@ -1127,14 +1127,18 @@ __device__ __forceinline__ int i8l_walk2(const i32x4* __restrict__ Al0, const i3
 // units 2^-38): 7 MFMAs per row block against 8.  Requires the diagonal form
 // (stage_i8o).
 // ---------------------------------------------------------------------------
-template <int NR, int WAVES, int OCC, int TT = 1>
+// MODE (fact_kernel 20, an experiment): 0 = prep and walk in one block (the
+// default); 1 = prep only, the evaluation's LDS image (G split, perm, digits)
+// copied out to img; 2 = walk only, the image copied in from img
+template <int NR, int WAVES, int OCC, int TT = 1, int MODE = 0>
 __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
     int S, int E, int ntiles, int nsets, int split, int cap, double padg,
     const int32_t* __restrict__ pos, const double* __restrict__ w01,
     const double* __restrict__ e_lo, const double* __restrict__ e_hi,
     const uint8_t* __restrict__ B8, const int8_t* __restrict__ udig, const double* __restrict__ u0,
     const double* __restrict__ nullsum, const void* __restrict__ tabs,
-    double* __restrict__ partial, double* __restrict__ ll_out, int remap) {
+    double* __restrict__ partial, double* __restrict__ ll_out, int remap,
+    int4* __restrict__ img = nullptr) {
   constexpr int SPAD = NR * 16;
   constexpr int NSL = 7;
   extern __shared__ __attribute__((aligned(16))) double lds8[];
@@ -1159,15 +1163,26 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int col = lane & 15, rg = lane >> 4;
 
+  constexpr int kImg4 = SPAD * 460 / 16;  // the image in int4: gi, perm, digits (i8img_bytes)
   {  // both tables (precomputed per context) in one contiguous 18 KB copy
+    // (the prep-only launch needs the log table alone)
     const int4* src = (const int4*)tabs;
     int4* dst = (int4*)lds8;
-    for (int k = tid; k < (kExpTabN * 8 + 128 * 16) / 16; k += blockDim.x) dst[k] = src[k];
-    for (int i = tid; i < SPAD; i += blockDim.x) {
-      elo_s[i] = i < S ? e_lo[i] : 1.0;
-      ehi_s[i] = i < S ? e_hi[i] : 1.0;
-    }
+    for (int k = tid + (MODE == 1 ? kExpTabN * 8 / 16 : 0); k < (kExpTabN * 8 + 128 * 16) / 16;
+         k += blockDim.x)
+      dst[k] = src[k];
+    if constexpr (MODE != 2)
+      for (int i = tid; i < SPAD; i += blockDim.x) {
+        elo_s[i] = i < S ? e_lo[i] : 1.0;
+        ehi_s[i] = i < S ? e_hi[i] : 1.0;
+      }
   }
+  if constexpr (MODE == 2) {
+    const int4* src = img + (size_t)b * kImg4;
+    int4* dst = (int4*)gi;
+    for (int k = tid; k < kImg4; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+  } else {
   i8_init_eval<SPAD, NSL, 4>(ev, pos + (size_t)b * S, S, tid, blockDim.x, padg);
   __syncthreads();
   {  // U' / ln 2 as the free diagonal "parent" i of child i
@@ -1197,6 +1212,13 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8l_kernel(
     gi[SPAD + i] = (int)rint(fma(g, kL2Scale, -g0) * 262144.0);
   }
   __syncthreads();
+  if constexpr (MODE == 1) {
+    const int4* src = (const int4*)gi;
+    int4* dst = img + (size_t)b * kImg4;
+    for (int k = tid; k < kImg4; k += blockDim.x) dst[k] = src[k];
+    return;
+  }
+  }  // MODE != 2
 #if NEMO_I8_ABLATE & 32  // instrumented build (tools/ablate.sh): prep only, no tiles
   if (s_end > 0) return;
 #endif
@@ -1677,7 +1699,7 @@ hipError_t launch_i8p_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   return hipGetLastError();
 }
 
-template <int NR, int WAVES, int OCC = NEMO_I8O_WAVES_PER_SIMD, int TT = 1>
+template <int NR, int WAVES, int OCC = NEMO_I8O_WAVES_PER_SIMD, int TT = 1, bool SPLIT = false>
 hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                         double* d_ll, hipStream_t st, int* nparts, bool* finalized) {
   constexpr int SPAD = NR * 16;
@@ -1687,9 +1709,20 @@ hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   int split = (slots + batch - 1) / batch;
   split = split < 1 ? 1 : (split > nsets ? nsets : split);
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + (size_t)7 * SPAD * 64;
-  score_i8l_kernel<NR, WAVES, OCC, TT><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
-      c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+  if (SPLIT) {  // fact_kernel 20: a prep-only launch (one block per evaluation), then the walks
+    if (!c.d_i8img || c.i8img_cap < batch || (size_t)SPAD * 460 != i8img_bytes(c.fspad))
+      return hipErrorInvalidValue;
+    score_i8l_kernel<NR, WAVES, OCC, TT, 1><<<dim3(batch), WAVES * kWave, lds, st>>>(
+        c.S, c.E, ntiles, nsets, 1, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap, (int4*)c.d_i8img);
+    score_i8l_kernel<NR, WAVES, OCC, TT, 2><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+        c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap, (int4*)c.d_i8img);
+  } else {
+    score_i8l_kernel<NR, WAVES, OCC, TT><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
+        c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+  }
   *nparts = nsets;
   *finalized = split == 1;
   return hipGetLastError();
@@ -2024,6 +2057,20 @@ __global__ __launch_bounds__(WAVES * kWave, OCC) void score_i8w_kernel(
 
 }  // namespace
 
+hipError_t i8img_reserve(Ctx& c) {
+  const int nb = std::max(c.cap_batch, 1);
+  if (c.d_i8img && c.i8img_cap >= nb) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(c.stream);
+  if (e != hipSuccess) return e;
+  ++c.graph_epoch;
+  if (c.d_i8img) (void)hipFree(c.d_i8img);
+  c.d_i8img = nullptr;
+  c.i8img_cap = 0;
+  e = hipMalloc((void**)&c.d_i8img, (size_t)nb * i8img_bytes(std::max(c.fspad, 16)));
+  if (e == hipSuccess) c.i8img_cap = nb;
+  return e;
+}
+
 hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01,
                             double* d_ll, int waves, bool l2, hipStream_t st, int* nparts,
                             bool* finalized) {
@@ -2039,6 +2086,7 @@ hipError_t launch_score_i8o(Ctx& c, int batch, int cap, const int32_t* d_pos, co
            : waves == 8  ? launch_i8l_t<NRV, 8>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized)  \
            : waves == -8 ? launch_i8l_t<NRV, 8, 6>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
            : waves == -2 ? launch_i8l_t<NRV, 8, NEMO_I8L2_OCC, 2>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
+           : waves == -20 ? launch_i8l_t<NRV, 8, NEMO_I8L2_OCC, 2, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \
                          : launch_i8l_t<NRV, 4>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized); \
     if (c.i8o_diag && !c.i8o_nodiag)                                                           \
       return waves == 8 ? launch_i8o_t<NRV, 8, true>(c, batch, cap, d_pos, d_w01, d_ll, st, nparts, finalized) \

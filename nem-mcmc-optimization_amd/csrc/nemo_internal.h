@@ -94,6 +94,10 @@ struct Ctx {
   bool i8l_ok = false;             // diagonal form and the fixed-point ranges hold
   int8_t* d_udig2 = nullptr;       // [S][8] digits of du_i / ln 2
   double* d_u0 = nullptr;          // [S] u0_i, added to G
+  // fact_kernel 20 (experiment): the prep's LDS image of each evaluation
+  // (G split, perm, digits) written by a prep-only launch, read by a walk-only one
+  int32_t* d_i8img = nullptr;      // [i8img_cap][i8l image]
+  int i8img_cap = 0;
   // the same for 64 < S <= 128 (score_i8w_kernel; d_B8 then holds two K halves)
   bool i8w_ok = false;
   double* d_nullsum_w = nullptr;   // [ceil(ntiles / 2)] sum of U[S][e] per 32 effects
@@ -157,6 +161,12 @@ struct Ctx {
 
   int ntiles() const { return (E + kTileCols - 1) / kTileCols; }
 };
+
+// fact_kernel 20: bytes of one evaluation's prep image (G split [2][SPAD]
+// int, perm [SPAD] int, digits [7][SPAD][64] bytes) and its buffer for the
+// reserved batch (allocated when the option is set or the batch grows)
+inline size_t i8img_bytes(int spad) { return (size_t)spad * 460; }
+hipError_t i8img_reserve(Ctx& c);
 
 // ---- launchers (nemo_kernels.hip); all enqueue on `st` and never allocate ----
 // exp() of the staged table (in place conversion from fp64 host layout)

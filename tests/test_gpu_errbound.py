@@ -121,3 +121,22 @@ def test_persistent_kernel_equals_default_past_its_grid():
     got = eng.score(pos, w01)
     assert np.array_equal(got, ref)
     eng.close()
+
+
+def test_split_prep_walk_equals_default():
+    """fact_kernel 20 (an experiment) runs kernel 10's prep and
+    walk as two launches, the prep's LDS image going through HBM: same bits
+    as kernel 10 at a split batch (B = 1, 16 blocks per evaluation), a ragged
+    one and past one block per CU; an image buffer grows with the batch."""
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(20)
+    for b in (1, 7, 1100):
+        pos = np.array([rng.permutation(64) for _ in range(b)], dtype=np.int32)
+        w01 = expit(rng.uniform(-3, 3, (b, 64, 64)))
+        eng.set_option("fact_kernel", 10)
+        ref = eng.score(pos, w01)
+        eng.set_option("fact_kernel", 20)
+        got = eng.score(pos, w01)
+        assert np.array_equal(got, ref), b
+    eng.close()
