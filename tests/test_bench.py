@@ -84,3 +84,15 @@ def test_kernel_tags():
 def test_cpu_baseline_procs_plumbing():
     r = bench.cpu_baseline_procs("C2", nproc=2, seconds=0.5)
     assert r["cores"] == 2 and r["kind"] == "port" and r["value"] > 0
+
+
+def test_stream_roofline_is_a_hardware_fraction():
+    # the streaming kernel's algorithmic bytes exceed HBM's (the table is
+    # Infinity-Cache resident and re-read across the batch): priced against
+    # the L2 read rate they give a fraction <= 1, HBM from the PMC record
+    bpe = bench.algorithmic_bytes_per_eval(64, 2000, 0, 8)
+    r = bench.stream_roofline(128, bpe, 0.2925, {"bytes_per_launch": 3.0e8})
+    assert r["bound"] == "l2" and 0.3 < r["frac"] <= 1.0
+    assert abs(r["achieved"] - 128 * bpe / 0.2925e-3 / 1e9) < 1e-6
+    assert 0.0 < r["secondary"]["hbm"]["frac"] <= 1.0 and r["traffic"] == 3.0e8
+    assert "secondary" not in bench.stream_roofline(128, bpe, 0.2925, None)

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd); P=${PROF_DIR:-gpurun_out/prof}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
 B=${NEMO_BENCH_BATCH:-2048}; CFG=${CONFIG:-C3}
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$P/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -${TAILN:-2} "$P/$name.log"; return $rc; }
-BENCH="$R/bench.py --config $CFG --batch $B --no-cpu-baseline"
+BENCH="$R/bench.py --config $CFG --batch $B --no-cpu-baseline ${BENCH_ARGS}"
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$P/trace" -o t -- python $BENCH --steps 20 --warmup 3 ${TRACE_ARGS:---no-extras} || exit 1
 step fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$P/fetch" -o f -- python $BENCH --steps 5 --warmup 1 --no-extras --warmup-seconds 0 || exit 1
 step write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$P/write" -o w -- python $BENCH --steps 5 --warmup 1 --no-extras --warmup-seconds 0 || exit 1
