@@ -229,6 +229,11 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *   "i8w"        (get only) 1 if the same is staged for 64 < S <= 128 (18 / 19)
  *   "graphs"     1 (default): nemo_optimal_weights replays its device work
  *                as a hipGraph per (nchains, cap); 0 = direct launches
+ *   "step_host_sum" 1 (default): nemo_optimal_weights (and _begin / _end)
+ *                copy eval #2's per-evaluation partials out with the other
+ *                outputs and sum them on the host in the device's fixed
+ *                order (same bits, one launch fewer); 0 = the device sums
+ *                them (as nemo_optimal_weights_dev always does)
  *   "local_split" 2 = run each local optimum of a fused step on a 4-wave
  *                block (the objective's products split over the waves; same
  *                bits; measured slower for one chain, so 0 = auto never

@@ -590,10 +590,20 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, 
 // ---------------------------------------------------------------------------
 // A6 fused per-step scorer
 // ---------------------------------------------------------------------------
-int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
-                             const double* d_anc, double sig0, double sig1, int cap,
-                             double* d_w_new, double* d_ll1, double* d_ll_dag, int32_t* d_info,
-                             void* stream) {
+}  // extern "C"
+
+namespace {
+
+// the fused step's device work on `stream`.  d_part2 null: eval #2's ll is
+// summed on the device into d_ll_dag.  Set (the staged host path): eval #2's
+// per-evaluation partials go to d_part2 (stride *np2) and are left for the
+// host (sum_partials_host, same bits), *np2 = their count -- one launch
+// fewer; *np2 = 0 when the kernel summed them itself (ll_dag written).
+int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
+                            const double* d_anc, double sig0, double sig1, int cap, double* d_w_new,
+                            double* d_ll1, double* d_ll_dag, int32_t* d_info, void* stream, double* d_part2,
+                            int* np2) {
+  if (np2) *np2 = 0;
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
   Ctx& c = ctx->c;
@@ -625,7 +635,13 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
   HIPCHK(nemo::launch_local_opt_pairs(c, nchains, npairs, c.d_pairs, c.d_rows, d_w01, d_anc, c.d_ow,
                                       sig0, sig1, d_w_new, c.d_wdag, d_info, st, fin));
   // eval #2 on the binarised weights (nem_order_mcmc.py:205-207)
-  if (use_factored(c)) {
+  if (use_factored(c) && d_part2) {
+    c.part_out = d_part2;
+    const hipError_t e = nemo::launch_score_factored(c, nchains, cap, d_pos, c.d_wdag, d_ll_dag, nullptr, nullptr,
+                                                     nullptr, st, false, np2);
+    c.part_out = nullptr;
+    HIPCHK(e);
+  } else if (use_factored(c)) {
     HIPCHK(nemo::launch_score_factored(c, nchains, cap, d_pos, c.d_wdag, d_ll_dag, nullptr, nullptr, nullptr, st));
   } else {
     HIPCHK(nemo::launch_prep(c, nchains, cap, d_pos, c.d_wdag, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
@@ -635,15 +651,32 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
   return NEMO_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
+                             const double* d_anc, double sig0, double sig1, int cap,
+                             double* d_w_new, double* d_ll1, double* d_ll_dag, int32_t* d_info,
+                             void* stream) {
+  return optimal_weights_enqueue(ctx, nchains, d_pos, d_w01, d_anc, sig0, sig1, cap, d_w_new, d_ll1, d_ll_dag,
+                                 d_info, stream, nullptr, nullptr);
+}
+
+}  // extern "C"
+
+namespace {
+
 // every transfer of a fused step goes through a pinned staging slot: [pos |
-// w01 | anc | w_new | info | ll1 | ll_dag], each part 256-B aligned, and a
-// device block with the same layout: one H2D of [pos .. anc], info preset to
-// -1 (= not a permissible pair) by the step's prep, one D2H of [w_new .. ll_dag];
-// the host hands back w_new at the entries info marks (the caller's values
-// stay everywhere else)
+// w01 | anc | w_new | info | ll1 | ll_dag | eval #2's partials], each part
+// 256-B aligned, and a device block with the same layout: one H2D of [pos ..
+// anc], info preset to -1 (= not a permissible pair) by the step's prep, one
+// D2H of [w_new .. partials]; the host hands back w_new at the entries info
+// marks (the caller's values stay everywhere else) and sums eval #2's
+// partials (npart: the most any score kernel writes per evaluation)
 struct StepLayout {
-  size_t o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, total;
-  StepLayout(size_t S, size_t n) {
+  size_t o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, o_part, total;
+  StepLayout(size_t S, size_t n, size_t npart) {
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
     o_w01 = up(n * S * 4);
     o_anc = o_w01 + up(n * S * S * 8);
@@ -651,9 +684,16 @@ struct StepLayout {
     o_inf = o_wn + up(n * S * S * 8);
     o_ll1 = o_inf + up(n * S * S * 4);
     o_lld = o_ll1 + up(n * 8);
-    total = o_lld + up(n * 8);
+    o_part = o_lld + up(n * 8);
+    total = o_part + up(n * npart * 8);
   }
 };
+
+size_t step_npart(const Ctx& c) { return use_factored(c) ? (size_t)nemo::factored_partials(c) : 0; }
+
+}  // namespace
+
+extern "C" {
 
 // first half of nemo_optimal_weights: validate, fill staging slot `slot`,
 // queue the device work (one H2D copy, the launches, one D2H copy) and record
@@ -670,7 +710,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
   const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
-  const StepLayout L(S, n);
+  const StepLayout L(S, n, step_npart(c));
   if ((rc = step_stage(c, slot, L.total))) return rc;
   char* hs = (char*)c.h_stage[slot];
   char* ds = (char*)c.d_step[slot];
@@ -680,12 +720,16 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   // replayed as a hipGraph per (nchains, cap, slot) while no captured
   // argument changes (the staging buffers, options and tables bump
   // graph_epoch), so a step costs one graph launch instead of ~10 API calls
+  int np2 = 0;
   auto enqueue = [&]() -> int {
     HIPCHK(hipMemcpyAsync(ds, hs, L.o_wn, hipMemcpyHostToDevice, st));  // info: preset by the prep
-    int r = nemo_optimal_weights_dev(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
-                                     (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
-                                     (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st);
+    int r = optimal_weights_enqueue(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
+                                    (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
+                                    (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st,
+                                    c.step_host_sum && L.o_part < L.total ? (double*)(ds + L.o_part) : nullptr,
+                                    &np2);
     if (r) return r;
+    if ((size_t)np2 * n * 8 > L.total - L.o_part) return fail(NEMO_ERR_STATE, "eval #2 partials exceed the slot");
     HIPCHK(hipMemcpyAsync(hs + L.o_wn, ds + L.o_wn, L.total - L.o_wn, hipMemcpyDeviceToHost, st));
     return NEMO_OK;
   };
@@ -714,6 +758,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
           g.sig0 = sig0;
           g.sig1 = sig1;
           g.epoch = c.graph_epoch;
+          g.np2 = np2;
           sg = &g;
         } else {
           g.exec = nullptr;
@@ -729,9 +774,11 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if (sg) {
     HIPCHK(hipGraphLaunch(sg->exec, st));
     c.ow_chains = nchains;  // nemo_optimal_weights_dev's host-side effect
+    np2 = sg->np2;
   } else if ((rc = enqueue())) {
     return rc;
   }
+  c.step_np2[slot] = np2;
   HIPCHK(hipEventRecord(c.step_done[slot], st));
   return NEMO_OK;
 }
@@ -743,11 +790,16 @@ static int step_finish(nemo_ctx* ctx, int slot, int nchains, double* w_new, doub
   Ctx& c = ctx->c;
   if (nchains == 0) return NEMO_OK;
   const size_t S = c.S, n = nchains;
-  const StepLayout L(S, n);
+  const StepLayout L(S, n, step_npart(c));
   HIPCHK(hipEventSynchronize(c.step_done[slot]));
   const char* hs = (const char*)c.h_stage[slot];
   memcpy(ll1, hs + L.o_ll1, n * 8);
-  memcpy(ll_dag, hs + L.o_lld, n * 8);
+  if (const int np2 = c.step_np2[slot]) {  // eval #2's partials: the device's fixed-order sum, on the host
+    const double* part = (const double*)(hs + L.o_part);
+    for (size_t b = 0; b < n; ++b) ll_dag[b] = nemo::host::sum_partials_host(part + b * (size_t)np2, np2);
+  } else {
+    memcpy(ll_dag, hs + L.o_lld, n * 8);
+  }
   if (info) memcpy(info, hs + L.o_inf, n * S * S * 4);
   const int32_t* inf = (const int32_t*)(hs + L.o_inf);
   const double* wn = (const double*)(hs + L.o_wn);
@@ -987,6 +1039,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.graphs = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "step_host_sum") == 0) {
+    ctx->c.step_host_sum = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "xcd_remap") == 0) {
     ctx->c.xcd_remap = value ? 1 : 0;
     return NEMO_OK;
@@ -1034,6 +1090,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "i8w") == 0) *value = c.i8w_ok ? 1 : 0;
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "graphs") == 0) *value = c.graphs;
+  else if (strcmp(name, "step_host_sum") == 0) *value = c.step_host_sum;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);

@@ -505,7 +505,7 @@ hipError_t launch_fact_w(Ctx& c, int batch, int cap, double* d_cs, double* d_cel
   const size_t lds = (size_t)SPAD * (KC + 1) * 8 + (size_t)SPAD * WPR * 8 + 64 * 8 + SPAD * 4;
   score_factored_kernel<NR, WAVES><<<dim3(nt * batch), WAVES * kWave, lds, st>>>(
       c.S, c.E, nt, cap, c.d_fDp, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
-      c.d_fpartial, d_cs, d_cells, d_ow, c.xcd_remap);
+      fpartial(c), d_cs, d_cells, d_ow, c.xcd_remap);
   *nparts = nt * WAVES;
   return hipGetLastError();
 }
@@ -532,7 +532,7 @@ hipError_t launch_pipe_t(Ctx& c, int batch, hipStream_t st, int* nparts) {
   const size_t lds = 256 * 8 + (size_t)SPAD * (SPAD + 2) * 8 + (size_t)nwb_max * SPAD * 8;
   score_factored_pipe_kernel<NR, WAVES><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, split, c.d_fDp, c.d_fperm, c.d_D1w, c.nwords, (const double*)c.d_U64,
-      c.d_fpartial, c.xcd_remap);
+      fpartial(c), c.xcd_remap);
   *nparts = split * WAVES;
   return hipGetLastError();
 }
@@ -687,7 +687,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // per-evaluation partials, summed in a fixed order
   if (defer_np) *defer_np = finalized ? 0 : np;
   else if (!finalized)
-    finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, c.d_fpartial, d_ll);
+    finalize_factored_kernel<<<(batch + 3) / 4, 256, 0, st>>>(batch, np, fpartial(c), d_ll);
   return hipGetLastError();
 }
 

@@ -614,7 +614,7 @@ hipError_t launch_i8_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const d
                sC = ldexp(1.0, c.i8_cexp - 60);
   score_i8_kernel<NR, WAVES, NP><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-      (const double*)c.d_U64, sA, sB, sC, c.d_fpartial, d_ll, c.xcd_remap);
+      (const double*)c.d_U64, sA, sB, sC, fpartial(c), d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
   return hipGetLastError();
@@ -913,7 +913,7 @@ hipError_t launch_i8o_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   const double sA = ldexp(1.0, c.i8_cexp - 24), sB = ldexp(1.0, c.i8_cexp - 48);
   score_i8o_kernel<NR, WAVES, DIAG><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8_cexp, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi,
-      c.d_B8, c.d_Uoff, c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB, c.d_fpartial, d_ll,
+      c.d_B8, c.d_Uoff, c.d_udig, c.d_u0, c.d_nullsum, c.d_i8o_tabs, sA, sB, fpartial(c), d_ll,
       c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
@@ -1661,7 +1661,7 @@ hipError_t launch_i8s_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   const size_t lds = kExpTabN * 8 + 128 * 16 + 3 * SPAD * 8 + 3 * SPAD * 4 + region;
   score_i8s_kernel<NR><<<dim3(batch * split), 8 * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, fpartial(c), d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = split == 1;
   return hipGetLastError();
@@ -1693,7 +1693,7 @@ hipError_t launch_i8p_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   const int grid = std::min(batch, 3 * ncu);
   score_i8p_kernel<NR, 8><<<dim3(grid), 8 * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, batch, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll);
+      c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, fpartial(c), d_ll);
   *nparts = nsets;
   *finalized = true;
   return hipGetLastError();
@@ -1714,14 +1714,14 @@ hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
       return hipErrorInvalidValue;
     score_i8l_kernel<NR, WAVES, OCC, TT, 1><<<dim3(batch), WAVES * kWave, lds, st>>>(
         c.S, c.E, ntiles, nsets, 1, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap, (int4*)c.d_i8img);
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, fpartial(c), d_ll, c.xcd_remap, (int4*)c.d_i8img);
     score_i8l_kernel<NR, WAVES, OCC, TT, 2><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
         c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap, (int4*)c.d_i8img);
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, fpartial(c), d_ll, c.xcd_remap, (int4*)c.d_i8img);
   } else {
     score_i8l_kernel<NR, WAVES, OCC, TT><<<dim3(batch * split), WAVES * kWave, lds, st>>>(
         c.S, c.E, ntiles, nsets, split, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8,
-        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+        c.d_udig2, c.d_u0, c.d_nullsum, c.d_i8o_tabs, fpartial(c), d_ll, c.xcd_remap);
   }
   *nparts = nsets;
   *finalized = split == 1;
@@ -2115,7 +2115,7 @@ hipError_t launch_i8w_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
   if (ae != hipSuccess) return ae;
   score_i8w_kernel<WAVES, 4, TWO><<<dim3(batch), WAVES * kWave, lds, st>>>(
       c.S, c.E, ntiles, nsets, cap, c.i8o_padg, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_B8, c.d_udig2, c.d_u0,
-      c.d_nullsum_w, c.d_i8o_tabs, c.d_fpartial, d_ll, c.xcd_remap);
+      c.d_nullsum_w, c.d_i8o_tabs, fpartial(c), d_ll, c.xcd_remap);
   *nparts = nsets;
   *finalized = true;
   return hipGetLastError();

@@ -257,6 +257,30 @@ inline bool build_inverse_schedule(InverseSchedule& sch, int S, int nprob, const
 }
 
 // ---------------------------------------------------------------------------
+// The device's fixed-order sum of an evaluation's n partials (sum_partials in
+// nemo_internal.h: lane l sums p[l], p[l + 64], ... in order, then six xor
+// butterfly stages, lane 0's value) restated on the host, operation for
+// operation: IEEE additions in the same order give the same bits.  The fused
+// step's staged path copies eval #2's partials out with its other outputs and
+// sums them here instead of in a finalize launch.
+// ---------------------------------------------------------------------------
+inline double sum_partials_host(const double* p, int n) {
+  constexpr int kLanes = 64;
+  double v[kLanes];
+  for (int l = 0; l < kLanes; ++l) {
+    double s = 0.0;
+    for (int t = l; t < n; t += kLanes) s += p[t];
+    v[l] = s;
+  }
+  for (int o = kLanes / 2; o >= 1; o >>= 1) {
+    double w[kLanes];
+    for (int l = 0; l < kLanes; ++l) w[l] = v[l] + v[l ^ o];
+    for (int l = 0; l < kLanes; ++l) v[l] = w[l];
+  }
+  return v[0];
+}
+
+// ---------------------------------------------------------------------------
 // Queue of asynchronous calls run in submission order on one library thread
 // (nemo_optimal_weights_begin / _end)
 // ---------------------------------------------------------------------------

@@ -74,6 +74,10 @@ struct Ctx {
   double* d_fG = nullptr;          // [cap][fspad]
   int32_t* d_fperm = nullptr;      // [cap][fspad]
   double* d_fpartial = nullptr;    // [cap][factored_partials]
+  // where the score kernels write their per-evaluation partials when set
+  // (fpartial()): the fused step's staged path points eval #2's at its
+  // staging block, so they ride in the one D2H copy and the host sums them
+  double* part_out = nullptr;
   // int8 matrix-core variant (S <= 64): fixed-point Delta digits
   int i8_cexp = 0;                 // per-model scale: 2^(c-1) >= max_j |hi_j - lo_j|
   uint8_t* d_B8 = nullptr;         // [2][KH][ceil(E/16)][64 lanes][16] D1 bytes in B-fragment order
@@ -136,17 +140,20 @@ struct Ctx {
   void* d_step[kStepSlots] = {};
   size_t d_step_bytes[kStepSlots] = {};
   hipEvent_t step_done[kStepSlots] = {};  // recorded after a slot's D2H copy
+  int step_np2[kStepSlots] = {};   // the slot's queued step: eval #2's partials per chain (host sums)
 
   // hipGraphs of nemo_optimal_weights' device work (one H2D copy, the
   // launches, one D2H copy) per (nchains, cap, sig0, sig1); graph_epoch moves
   // whenever a captured argument may change (buffers, options, staging)
   struct StepGraph {
     int nchains = -1, cap = -1, slot = -1;
+    int np2 = 0;                   // eval #2's partials per chain left for the host (0: ll_dag on device)
     double sig0 = 0.0, sig1 = 0.0;
     uint64_t epoch = 0;
     hipGraphExec_t exec = nullptr;
   };
   int graphs = 1;                  // option "graphs": replay the fused step as a hipGraph
+  int step_host_sum = 1;           // option "step_host_sum": the staged step sums eval #2's partials on the host
   uint64_t graph_epoch = 1;
   static constexpr int kStepGraphs = 8;
   StepGraph step_graph[kStepGraphs];
@@ -161,6 +168,9 @@ struct Ctx {
 
   int ntiles() const { return (E + kTileCols - 1) / kTileCols; }
 };
+
+// the partial buffer the score kernels write (Ctx::part_out over d_fpartial)
+inline double* fpartial(const Ctx& c) { return c.part_out ? c.part_out : c.d_fpartial; }
 
 // fact_kernel 20: bytes of one evaluation's prep image (G split [2][SPAD]
 // int, perm [SPAD] int, digits [7][SPAD][64] bytes) and its buffer for the

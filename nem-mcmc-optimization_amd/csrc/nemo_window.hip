@@ -384,7 +384,7 @@ hipError_t launch_window2_t(Ctx& c, int batch, int cap, const int32_t* d_pos, co
   }
   score_window2_kernel<NB, kWinWaves><<<dim3(batch * split), kWinWaves * kWave, lds, st>>>(
       c.S, c.E, c.nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
-      c.d_fpartial, d_ll);
+      fpartial(c), d_ll);
   return hipGetLastError();
 }
 
@@ -423,7 +423,7 @@ hipError_t launch_score_window(Ctx& c, int batch, int cap, const int32_t* d_pos,
   }
   score_window_kernel<kWinWaves><<<dim3(batch * split), kWinWaves * kWave, lds1, st>>>(
       c.S, c.E, nwords, cap, split, d_pos, d_w01, c.d_elo, c.d_ehi, c.d_D1w, c.d_wuw, c.d_wnull,
-      c.d_fpartial, d_ll);
+      fpartial(c), d_ll);
   *nparts = nwords;
   *finalized = split == 1;
   return hipGetLastError();

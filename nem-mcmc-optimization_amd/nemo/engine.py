@@ -307,8 +307,10 @@ class _OptimalWeightsCall:
         self.info = np.empty((n, s, s), dtype=np.int32)
         self._keep = (pos, w01, anc)
         self._fn = _lib.load().nemo_optimal_weights
-        self._args = (eng._ctx, n, ptr(pos, _lib._i32p), ptr(w01), ptr(anc), float(sig0), float(sig1),
-                      int(cap), ptr(self.w_new), ptr(self.ll1), ptr(self.lld), ptr(self.info, _lib._i32p))
+        # (the arrays stay referenced by this object for the call's lifetime)
+        a = _lib.addr
+        self._args = (eng._ctx, n, a(pos), a(w01), a(anc), float(sig0), float(sig1),
+                      int(cap), a(self.w_new), a(self.ll1), a(self.lld), a(self.info))
         self.rc = None
 
     def run(self):

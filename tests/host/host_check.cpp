@@ -373,6 +373,34 @@ static void check_step_queue(std::mt19937_64& rng) {
   check_pipelined_queue(rng);
 }
 
+// ---- the device's fixed-order partial sum on the host ------------------------
+// sum_partials_host restates sum_partials (nemo_internal.h): 64 strided lane
+// sums, then xor butterflies with o = 32, 16, ..., 1, lane 0's value.  Checked
+// against the same tree written backwards as a recursion: lane l's value
+// after the stages down to o is its value and lane (l ^ o)'s after the stages
+// down to 2o, added.  Values whose sums round, so another association shows.
+static double after_stages(const double* lanes, int l, int o) {
+  if (o == 64) return lanes[l];
+  return after_stages(lanes, l, 2 * o) + after_stages(lanes, l ^ o, 2 * o);
+}
+static void check_sum_partials(std::mt19937_64& rng) {
+  std::uniform_real_distribution<double> u(-1e3, 1e3);
+  for (int n : {0, 1, 5, 63, 64, 65, 127, 200, 1000}) {
+    std::vector<double> p(n);
+    for (auto& x : p) x = u(rng) * (1.0 + 1e-9 * u(rng));
+    double lanes[64];
+    for (int l = 0; l < 64; ++l) {
+      double s = 0.0;
+      for (int t = l; t < n; t += 64) s += p[t];
+      lanes[l] = s;
+    }
+    CHECK(sum_partials_host(p.data(), n) == after_stages(lanes, 0, 1));
+  }
+  const double small[3] = {1.0, 2.0, 3.0};
+  CHECK(sum_partials_host(small, 3) == 6.0);
+  CHECK(sum_partials_host(small, 0) == 0.0);
+}
+
 int main() {
   std::mt19937_64 rng(20261017);
   check_pos_rows();
@@ -380,6 +408,7 @@ int main() {
   check_bounds(rng);
   check_inverse_schedule(rng);
   check_step_queue(rng);
+  check_sum_partials(rng);
   printf("ok %d\n", g_checks);
   return 0;
 }

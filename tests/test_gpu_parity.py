@@ -803,3 +803,39 @@ def test_chain_checkpoint_resume_equals_one_run(tmp_path):
     assert np.array_equal(b3, b1)
     with pytest.raises(ValueError, match="resume"):
         ChainBatch(m, orders, seeds, engine=one.engine).run(1, resume=True)
+
+
+@pytest.mark.parametrize("n,cap", [(1, 0), (3, 0), (2, 5), (600, 0)])
+def test_fused_step_host_summed_ll_dag_equals_device_sum(n, cap):
+    """The staged fused step (nemo_optimal_weights) copies eval #2's partials
+    out with its other outputs and sums them on the host (sum_partials_host,
+    nemo_host.h) instead of in a finalize launch; nemo_optimal_weights_dev
+    keeps the device's sum.  Same bits: one chain (16 blocks, partials per set),
+    a ragged group, a capped call (the lookup-table kernel's per-word
+    partials) and a batch past the split (the kernel sums in-kernel)."""
+    import ctypes as C
+    import torch
+    from nemo import _lib
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(90 + n)
+    pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
+    w = rng.uniform(-3, 3, (n, 64, 64))
+    anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
+    w_new, ll1, lld, info = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, cap=cap, raise_on_fail=False)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    dp, dw, da = dev(pos), dev(expit(w)), dev(anc)
+    dn = torch.zeros((n, 64, 64), dtype=torch.float64, device="cuda")
+    d1 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    d2 = torch.zeros(n, dtype=torch.float64, device="cuda")
+    di = torch.zeros((n, 64, 64), dtype=torch.int32, device="cuda")
+    rc = _lib.load().nemo_optimal_weights_dev(eng._ctx, n, C.c_void_p(dp.data_ptr()), C.c_void_p(dw.data_ptr()),
+                                             C.c_void_p(da.data_ptr()), SIG0, SIG1, cap, C.c_void_p(dn.data_ptr()),
+                                             C.c_void_p(d1.data_ptr()), C.c_void_p(d2.data_ptr()),
+                                             C.c_void_p(di.data_ptr()), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(d2.cpu().numpy(), lld)
+    assert np.array_equal(d1.cpu().numpy(), ll1)
+    eng.close()

@@ -39,3 +39,16 @@ def dev10():
         lib.nemo_optimal_weights_dev(eng._ctx, n, C.c_void_p(dp.data_ptr()), C.c_void_p(dw.data_ptr()), C.c_void_p(da.data_ptr()), SIG0, SIG1, 0, C.c_void_p(dn.data_ptr()), C.c_void_p(d1.data_ptr()), C.c_void_p(d2.data_ptr()), C.c_void_p(di.data_ptr()), C.c_void_p(st))
     torch.cuda.synchronize()
 print("dev x10 / 10", med(dev10, 10) / 10)
+# A/B of one option on the synchronous staged call, interleaved (AB_OPT=name:
+# rounds of 30 calls with the option at 0 and 1 in turn; medians per value)
+if os.environ.get("AB_OPT"):
+    name = os.environ["AB_OPT"]
+    res = {0: [], 1: []}
+    for _ in range(7):
+        for v in (0, 1):
+            eng.set_option(name, v)
+            raw()  # first call after an option change captures a new graph
+            res[v].append(med(raw))
+    for v in (0, 1):
+        print(f"AB {name}={v} raw ctypes median of rounds {np.median(res[v]):.5f} ms, rounds {np.round(res[v], 5).tolist()}")
+    eng.set_option(name, 1)
