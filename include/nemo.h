@@ -237,7 +237,7 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *   "local_split" 2 = run each local optimum of a fused step on a 4-wave
  *                block (the objective's products split over the waves; same
  *                bits; measured slower for one chain, so 0 = auto never
- *                takes it), 1 = never */
+ *                takes it), 1 = never, 3 = the same on a 2-wave block */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

@@ -1063,7 +1063,7 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "local_split") == 0) {
-    if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "local_split=%d not in {0,1,2}", value);
+    if (value < 0 || value > 3) return fail(NEMO_ERR_ARG, "local_split=%d not in {0,1,2,3}", value);
     ctx->c.local_split = value;
     return NEMO_OK;
   }

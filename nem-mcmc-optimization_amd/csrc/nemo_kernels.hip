@@ -567,16 +567,21 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
 // objective (~430 instructions per f-evaluation at NPL = 32) alone: split,
 // each wave issues a quarter of the products.  Posts are double-buffered, so
 // one barrier per f-evaluation suffices.
-template <int NPL>
+// NW = 2 (option local_split 3): two waves per problem, each multiplying half
+// the chains, and the last tree level over the two posts -- the same tree, so
+// the same bits -- at half the waves of the 4-wave form (4032 for one C3
+// chain, which fit the chip at once; the 4-wave form's 8064 do not).
+template <int NPL, int NW = 4>
 struct SplitObjective {
   static constexpr int NC = NPL / 4;  // chains of LocalObjective
-  static constexpr int L = NC / 4;    // chains per wave (a power of 2)
-  static_assert(L == 1 || L == 2 || L == 4, "split objective: NPL in {16, 32, 64}");
+  static constexpr int L = NC / NW;   // chains per wave (a power of 2)
+  static_assert((NW == 4 || NW == 2) && (L == 1 || L == 2 || L == 4 || L == 8),
+                "split objective: NPL in {16, 32, 64}, 2 or 4 waves");
   double c[4 * L];                    // this lane's elements 4 L w .. 4 L w + 4 L - 1
   double anc;
   const double2* ltab;
-  double2* post;                      // LDS [2 buffers][4 waves][64 lanes] (m(x0), m(x1))
-  int2* kpost;                        // LDS [2][4][64] (k(x0), k(x1))
+  double2* post;                      // LDS [2 buffers][NW waves][64 lanes] (m(x0), m(x1))
+  int2* kpost;                        // LDS [2][NW][64] (k(x0), k(x1))
   int w, lane;
   mutable int par = 0;
   __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
@@ -607,19 +612,31 @@ struct SplitObjective {
         m0[u] *= m0[u + wd];
         m1[u] *= m1[u + wd];
       }
-    const int slot = (par * 4 + w) * kWave + lane;
+    const int slot = (par * NW + w) * kWave + lane;
     post[slot] = double2{m0[0], m1[0]};
     kpost[slot] = int2{k0, k1};
     __syncthreads();
-    const int base = par * 4 * kWave + lane;
-    const double2 q0 = post[base], q1 = post[base + kWave], q2 = post[base + 2 * kWave],
-                  q3 = post[base + 3 * kWave];
-    const int2 j0 = kpost[base], j1 = kpost[base + kWave], j2 = kpost[base + 2 * kWave],
-               j3 = kpost[base + 3 * kWave];
+    const int base = par * NW * kWave + lane;
+    double r0, r1;
+    int kk0, kk1;
+    if constexpr (NW == 4) {
+      const double2 q0 = post[base], q1 = post[base + kWave], q2 = post[base + 2 * kWave],
+                    q3 = post[base + 3 * kWave];
+      const int2 j0 = kpost[base], j1 = kpost[base + kWave], j2 = kpost[base + 2 * kWave],
+                 j3 = kpost[base + 3 * kWave];
+      r0 = (q0.x * q1.x) * (q2.x * q3.x);
+      r1 = (q0.y * q1.y) * (q2.y * q3.y);
+      kk0 = j0.x + j1.x + j2.x + j3.x;
+      kk1 = j0.y + j1.y + j2.y + j3.y;
+    } else {
+      const double2 q0 = post[base], q1 = post[base + kWave];
+      const int2 j0 = kpost[base], j1 = kpost[base + kWave];
+      r0 = q0.x * q1.x;
+      r1 = q0.y * q1.y;
+      kk0 = j0.x + j1.x;
+      kk1 = j0.y + j1.y;
+    }
     par ^= 1;
-    double r0 = (q0.x * q1.x) * (q2.x * q3.x);
-    double r1 = (q0.y * q1.y) * (q2.y * q3.y);
-    int kk0 = j0.x + j1.x + j2.x + j3.x, kk1 = j0.y + j1.y + j2.y + j3.y;
     kk0 += __builtin_amdgcn_frexp_exp(r0);
     kk1 += __builtin_amdgcn_frexp_exp(r1);
     r0 = __builtin_amdgcn_frexp_mant(r0);
@@ -635,16 +652,16 @@ struct SplitObjective {
 
 // local_opt_pairs_kernel with one (chain, pair) per 4-wave block
 // (SplitObjective): the same results bit for bit.  grid = nchains * npairs.
-template <typename TT, int NPL>
-__global__ __launch_bounds__(256) void local_opt_pairs_split_kernel(
+template <typename TT, int NPL, int NW = 4>
+__global__ __launch_bounds__(NW * kWave) void local_opt_pairs_split_kernel(
     int S, int E, int npairs, int nchains, const TT* __restrict__ eT,
     const int32_t* __restrict__ pairs, const int32_t* __restrict__ rows,
     const double* __restrict__ w01, const double* __restrict__ anc, const double* __restrict__ ow,
     double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
     int32_t* __restrict__ info) {
   __shared__ double2 ltab[128];
-  __shared__ double2 post[2 * 4 * kWave];
-  __shared__ int2 kpost[2 * 4 * kWave];
+  __shared__ double2 post[2 * NW * kWave];
+  __shared__ int2 kpost[2 * NW * kWave];
   fill_log_table(ltab, threadIdx.x, blockDim.x);
   __syncthreads();
   const int gp = blockIdx.x;  // one problem per block
@@ -660,7 +677,7 @@ __global__ __launch_bounds__(256) void local_opt_pairs_split_kernel(
   const double s = w01[idx];
   const TT* tv = eT + ((size_t)i * S + k) * E;
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
-  using Obj = SplitObjective<NPL>;
+  using Obj = SplitObjective<NPL, NW>;
   Obj obj;
   obj.ltab = ltab;
   obj.post = post;
@@ -872,11 +889,23 @@ static hipError_t local_pairs_t(Ctx& c, int nchains, int npairs, const int32_t* 
   // bits); option "local_split": 0 auto, 1 never, 2 always (where it applies)
   const int npl = npl_for(c.E);
   const bool splittable = prod && (npl == 16 || npl == 32 || npl == 64);
-  const bool split = splittable && (c.local_split == 2 || (c.local_split == 0 && waves <= (size_t)kLocalSplitMax));
+  const bool split = splittable && (c.local_split >= 2 || (c.local_split == 0 && waves <= (size_t)kLocalSplitMax));
   if (split) {
     if (fin.ll)
       finalize_factored_sums<<<(fin.batch + 3) / 4, 256, 0, st>>>(fin);
     const int nb = (int)waves;
+    if (c.local_split == 3) {  // two waves per problem
+      if (npl == 16)
+        local_opt_pairs_split_kernel<TT, 16, 2><<<nb, 128, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                                   d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+      else if (npl == 32)
+        local_opt_pairs_split_kernel<TT, 32, 2><<<nb, 128, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                                   d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+      else
+        local_opt_pairs_split_kernel<TT, 64, 2><<<nb, 128, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
+                                                                   d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);
+      return hipGetLastError();
+    }
     if (npl == 16)
       local_opt_pairs_split_kernel<TT, 16><<<nb, 256, 0, st>>>(c.S, c.E, npairs, nchains, eT, d_pairs, d_rows,
                                                               d_w01, d_anc, d_ow, sig0, sig1, d_wnew, d_wdag, d_info);

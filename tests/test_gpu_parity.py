@@ -715,8 +715,8 @@ def test_queued_fused_step_equals_direct_call():
 
 @pytest.mark.parametrize("n", [1, 3])
 def test_split_local_optima_same_bits(n):
-    """The fused step's local optima on 4-wave blocks (local_split 2, what auto
-    takes for a few chains) give exactly the one-wave kernel's results."""
+    """The fused step's local optima on 4-wave and 2-wave blocks (local_split 2
+    and 3) give exactly the one-wave kernel's results."""
     from nemo.nem_order_mcmc import SIG0, SIG1
     m = generator.synthetic_nem(64, 2000, 0)
     eng = Engine.for_nem(m)
@@ -725,10 +725,10 @@ def test_split_local_optima_same_bits(n):
     w = rng.uniform(-3, 3, (n, 64, 64))
     anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
     out = {}
-    for mode in (1, 2, 0):
+    for mode in (1, 2, 3, 0):
         eng.set_option("local_split", mode)
         out[mode] = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
-    for mode in (2, 0):
+    for mode in (2, 3, 0):
         for x, y in zip(out[mode], out[1]):
             assert np.array_equal(x, y), mode
     eng.set_option("local_split", 0)

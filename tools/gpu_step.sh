@@ -5,6 +5,6 @@ P=${PROF_DIR:-gpurun_out/step}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFER
 step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$P/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -${TAILN:-6} "$P/$name.log"; return $rc; }
 TAILN=8 step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS} || exit 1
 step probe1 200 python tools/step_probe.py 1 || exit 1
-AB_OPT=step_host_sum step probe1b 300 python tools/step_probe.py 1 || exit 1
-AB_OPT=step_host_sum step probe4 300 python tools/step_probe.py 4 || exit 1
+AB_OPT=local_split AB_VALS=1,3,2 step probe1ab 400 python tools/step_probe.py 1 || exit 1
+AB_OPT=local_split AB_VALS=1,3 step probe4ab 400 python tools/step_probe.py 4 || exit 1
 step probe16 200 python tools/step_probe.py 16 || exit 1

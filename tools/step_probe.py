@@ -43,12 +43,13 @@ print("dev x10 / 10", med(dev10, 10) / 10)
 # rounds of 30 calls with the option at 0 and 1 in turn; medians per value)
 if os.environ.get("AB_OPT"):
     name = os.environ["AB_OPT"]
-    res = {0: [], 1: []}
+    vals = [int(v) for v in os.environ.get("AB_VALS", "0,1").split(",")]
+    res = {v: [] for v in vals}
     for _ in range(7):
-        for v in (0, 1):
+        for v in vals:
             eng.set_option(name, v)
             raw()  # first call after an option change captures a new graph
             res[v].append(med(raw))
-    for v in (0, 1):
+    for v in vals:
         print(f"AB {name}={v} raw ctypes median of rounds {np.median(res[v]):.5f} ms, rounds {np.round(res[v], 5).tolist()}")
-    eng.set_option(name, 1)
+    eng.set_option(name, vals[-1])
