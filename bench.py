@@ -437,7 +437,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=8,
                     help="processes of the multi-process CPU baseline (1: off)")
     ap.add_argument("--c4-chains", type=int, default=128, help="C4: chains over all ranks (0: off)")
-    ap.add_argument("--c4-steps", type=int, default=10, help="C4: timed MCMC steps")
+    ap.add_argument("--c4-steps", type=int, default=30, help="C4: timed MCMC steps (after 2 untimed ones)")
     args = ap.parse_args()
 
     import torch
