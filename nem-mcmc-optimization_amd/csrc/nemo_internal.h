@@ -378,7 +378,8 @@ __device__ __forceinline__ void prep_order_lds(int S, int cap, const int32_t* __
 
 // one wave: child i's permissible parents in pi order (nem_order_mcmc.py:
 // 62-65; with cap, the last `cap` of them), their weights, the list length,
-// the child's slots of the flat pair list (when pairs), and -1 in every entry
+// the child's slots of the flat pair list (when pairs: i << 16 | parent
+// node, in list order), and -1 in every entry
 // of its info row (when info: "not a permissible pair"; the local optima
 // overwrite theirs)
 __device__ __forceinline__ void prep_child_list(int S, int cap, const int32_t* __restrict__ pb,
@@ -401,7 +402,7 @@ __device__ __forceinline__ void prep_child_list(int S, int cap, const int32_t* _
     const int j = perm[lo + t];
     r[t] = j;
     w[t] = wr[j];
-    if (pr) pr[t] = (i << 16) | t;
+    if (pr) pr[t] = (i << 16) | j;  // the parent node itself: no rows[] lookup in the consumers
   }
   if (lane == 0) cnt[(size_t)b * S + i] = n;
 }

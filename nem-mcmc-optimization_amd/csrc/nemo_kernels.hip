@@ -522,18 +522,22 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
   const int n = gw - b * npairs;
   const int pk = pairs[(size_t)b * S * S + n];
   const int i = pk >> 16;
-  const int t = pk & 0xffff;
-  const int k = rows[((size_t)b * S + i) * S + t];
+  const int k = pk & 0xffff;  // the parent node (prep_child_list)
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
   const TT* tv = eT + ((size_t)i * S + k) * E;
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   LocalObjective<NPL, PROD> obj;
   obj.ltab = ltab;
+  // every lane loads (a clamped index past E) and divides, then padding is
+  // selected away: no branch per element, so the 2 NPL loads and the NPL
+  // divisions of the setup overlap instead of running one after another
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
     const int e = q * kWave + lane;
-    obj.c[q] = (e < E) ? local_c((double)tv[e], owk[e], s) : 0.0;  // padding: log(1) = 0
+    const int ec = e < E ? e : E - 1;
+    const double v = local_c((double)tv[ec], owk[ec], s);
+    obj.c[q] = (e < E) ? v : 0.0;  // padding: log(1) = 0
   }
   obj.anc = anc[idx];
 #ifdef NEMO_LO_TRACE
@@ -671,8 +675,7 @@ __global__ __launch_bounds__(NW * kWave) void local_opt_pairs_split_kernel(
   const int n = gp - b * npairs;
   const int pk = pairs[(size_t)b * S * S + n];
   const int i = pk >> 16;
-  const int t = pk & 0xffff;
-  const int k = rows[((size_t)b * S + i) * S + t];
+  const int k = pk & 0xffff;  // the parent node (prep_child_list)
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
   const TT* tv = eT + ((size_t)i * S + k) * E;
@@ -685,9 +688,11 @@ __global__ __launch_bounds__(NW * kWave) void local_opt_pairs_split_kernel(
   obj.w = w;
   obj.lane = lane;
 #pragma unroll
-  for (int q = 0; q < 4 * Obj::L; ++q) {
+  for (int q = 0; q < 4 * Obj::L; ++q) {  // (branch-free setup as in local_opt_pairs_kernel)
     const int e = (4 * Obj::L * w + q) * kWave + lane;
-    obj.c[q] = (e < E) ? local_c((double)tv[e], owk[e], s) : 0.0;  // padding: log(1) = 0
+    const int ec = e < E ? e : E - 1;
+    const double v = local_c((double)tv[ec], owk[ec], s);
+    obj.c[q] = (e < E) ? v : 0.0;  // padding: log(1) = 0
   }
   obj.anc = anc[idx];
   const LbfgsResult r = lbfgsb1_minimize(obj, s);
@@ -715,7 +720,8 @@ __global__ __launch_bounds__(256) void local_opt_generic_kernel(
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
     const int e = q * kWave + lane;
-    obj.c[q] = (e < E) ? cvec[(size_t)gw * E + e] : 0.0;
+    const double v = cvec[(size_t)gw * E + (e < E ? e : E - 1)];  // branch-free: clamped, then selected
+    obj.c[q] = (e < E) ? v : 0.0;
   }
   obj.anc = anc[gw];
   const LbfgsResult r = lbfgsb1_minimize(obj, x0[gw]);

@@ -78,8 +78,7 @@ __global__ __launch_bounds__(256) void gamma_pairs_kernel(
   const int n = gw - b * npairs;
   const int pk = pairs[(size_t)b * S * S + n];
   const int i = pk >> 16;
-  const int t = pk & 0xffff;
-  const int k = rows[((size_t)b * S + i) * S + t];
+  const int k = pk & 0xffff;  // the parent node (prep_child_list)
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w[idx];
   const TT* tv = eT + ((size_t)i * S + k) * E;
@@ -88,16 +87,19 @@ __global__ __launch_bounds__(256) void gamma_pairs_kernel(
   obj.ltab = ltab;
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
+    // branch-free setup (a clamped index past E, padding selected away), so
+    // the loads and divisions of all elements overlap
     const int e = q * kWave + lane;
-    double cv = 0.0;  // padding: log(1) = 0, c/(1) = 0
-    if (e < E) {
+    const int ec = e < E ? e : E - 1;
+    double cv;
+    {
 #pragma clang fp contract(off)
-      const double lv = (double)tv[e];
-      const double a = (lv - 1.0) * owk[e];
+      const double lv = (double)tv[ec];
+      const double a = (lv - 1.0) * owk[ec];
       const double bb = (1.0 - s * a) + s * (lv - 1.0);
       cv = a / bb;
     }
-    obj.c[q] = cv;
+    obj.c[q] = e < E ? cv : 0.0;  // padding: log(1) = 0, c/(1) = 0
   }
   LbOpts o;
   o.lo = 0.0;
