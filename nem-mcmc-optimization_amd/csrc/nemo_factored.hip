@@ -243,10 +243,25 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
 
   const double* Db = Dp + (size_t)b * SPAD * SPAD;
   constexpr int NCH = SPAD / KC;
+  // the epilogue's U values, loaded once perm_s is visible (the first chunk's
+  // barrier) so their latency hides behind the staging and the MFMAs instead
+  // of following them (a lone evaluation's launch is a chain of such waits)
+  double uv[NR][4];
+  double unull = 0.0;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int c0 = c * KC;
     __syncthreads();
+    if (c == 0) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int q = 16 * r + (lane >> 4) + 4 * g;
+          uv[r][g] = q < S ? U[(size_t)perm_s[q] * E + ec] : 0.0;
+        }
+      unull = U[(size_t)S * E + ec];
+    }
     // stage Delta[:, c0 .. c0+KC) (coalesced rows); only rows that have
     // parents in this chunk (row q needs p < q, i.e. q > c0)
     for (int k = tid; k < SPAD * KC; k += blockDim.x) {
@@ -291,12 +306,11 @@ __global__ __launch_bounds__(WAVES * kWave) void score_factored_kernel(
     for (int g = 0; g < 4; ++g) {
       const int q = 16 * r + (lane >> 4) + 4 * g;
       double v = -INFINITY;
-      if (q < S) v = U[(size_t)perm_s[q] * E + ec] + acc[r][g];
+      if (q < S) v = uv[r][g] + acc[r][g];
       cell[r][g] = v;
       m = v > m ? v : m;
     }
   }
-  const double unull = U[(size_t)S * E + ec];
   m = m > unull ? m : unull;
   m = fmax(m, __shfl_xor(m, 16, kWave));
   m = fmax(m, __shfl_xor(m, 32, kWave));
