@@ -397,11 +397,11 @@ struct LocalObjective {
       constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;
       constexpr double kLn2Lo = 5.4956039718945254e-14;
       // NC independent chains of 4 factors (chain u: elements 4u .. 4u + 3 of
-      // the lane), each renormalised once by frexp, then the mantissas
-      // multiplied in a fixed pairwise tree: the dependent chain of an
-      // f-evaluation (the line search's serial path) is 4 + log2(NC) products
-      // instead of NPL.  4 factors stay in [e^-320, e^320] for |T| <= 40, a
-      // product of <= 32 mantissas in [0.5, 1) stays normal.
+      // the lane) multiplied in a fixed pairwise tree, renormalised by frexp
+      // after its first level: the dependent chain of an f-evaluation (the
+      // line search's serial path) is 4 + log2(NC) products instead of NPL.
+      // A factor lies in [e^-80, e^80] for |T| <= 40, so 8 of them stay
+      // normal, and a product of <= 16 mantissas in [0.5, 1) too.
       constexpr int NC = NPL / 4;
       double m0[NC], m1[NC];
       int k0 = 0, k1 = 0;
@@ -415,13 +415,31 @@ struct LocalObjective {
           a0 *= fma(c[4 * u + v], e0, 1.0);
           a1 *= fma(c[4 * u + v], e1, 1.0);
         }
-        k0 += __builtin_amdgcn_frexp_exp(a0);
-        m0[u] = __builtin_amdgcn_frexp_mant(a0);
-        k1 += __builtin_amdgcn_frexp_exp(a1);
-        m1[u] = __builtin_amdgcn_frexp_mant(a1);
+        m0[u] = a0;
+        m1[u] = a1;
+      }
+      // the tree's first level multiplies two chains' raw products (8 factors
+      // in [e^-640, e^640]: normal, so the rounding is that of their mantissas'
+      // product), then renormalises: half the frexps of renormalising every
+      // chain, and the same bits (an exact power of 2 never changes a
+      // product's rounding); deeper levels multiply mantissas in [0.5, 1)
+      if constexpr (NC == 1) {
+        k0 += __builtin_amdgcn_frexp_exp(m0[0]);
+        m0[0] = __builtin_amdgcn_frexp_mant(m0[0]);
+        k1 += __builtin_amdgcn_frexp_exp(m1[0]);
+        m1[0] = __builtin_amdgcn_frexp_mant(m1[0]);
       }
 #pragma unroll
-      for (int wd = 1; wd < NC; wd *= 2)
+      for (int u = 0; u + 1 < NC; u += 2) {
+        m0[u] *= m0[u + 1];
+        m1[u] *= m1[u + 1];
+        k0 += __builtin_amdgcn_frexp_exp(m0[u]);
+        m0[u] = __builtin_amdgcn_frexp_mant(m0[u]);
+        k1 += __builtin_amdgcn_frexp_exp(m1[u]);
+        m1[u] = __builtin_amdgcn_frexp_mant(m1[u]);
+      }
+#pragma unroll
+      for (int wd = 2; wd < NC; wd *= 2)
 #pragma unroll
         for (int u = 0; u + wd < NC; u += 2 * wd) {
           m0[u] *= m0[u + wd];
