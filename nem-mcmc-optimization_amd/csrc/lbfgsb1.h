@@ -42,6 +42,12 @@ constexpr double kStpMax = 1e10;
 constexpr double kFtolLs = 1e-3, kGtolLs = 0.9, kXtolLs = 0.1;
 
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+
+// A branch of the optimiser's control flow: its condition is wave-uniform
+// (every lane holds the same f, g and state), so the first lane decides and
+// the compiler emits a scalar branch -- no exec-mask save / restore and no
+// divergent-merge copies of the ~30 state values per branch.
+__device__ __forceinline__ bool uni(bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
 
 // MINPACK-2 dcstep: safeguarded step and interval update.
@@ -51,7 +57,7 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
 #pragma clang fp contract(off)
   const double sgnd = dp * (dx / fabs(dx));
   double stpf;
-  if (fp > fx) {
+  if (uni(fp > fx)) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -64,7 +70,7 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
     const double stpq = stx + ((dx / ((fx - fp) / (stp - stx) + dx)) / 2.0) * (stp - stx);
     stpf = (fabs(stpc - stx) < fabs(stpq - stx)) ? stpc : stpc + (stpq - stpc) / 2.0;
     brackt = true;
-  } else if (sgnd < 0.0) {
+  } else if (uni(sgnd < 0.0)) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -77,7 +83,7 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
     const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
     stpf = (fabs(stpc - stp) > fabs(stpq - stp)) ? stpc : stpq;
     brackt = true;
-  } else if (fabs(dp) < fabs(dx)) {
+  } else if (uni(fabs(dp) < fabs(dx))) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -91,7 +97,7 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
     else if (stp > stx) stpc = stpmax;
     else stpc = stpmin;
     const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
-    if (brackt) {
+    if (uni(brackt)) {
       stpf = (fabs(stpc - stp) < fabs(stpq - stp)) ? stpc : stpq;
       if (stp > stx) stpf = dmin(stp + 0.66 * (sty - stp), stpf);
       else stpf = dmax(stp + 0.66 * (sty - stp), stpf);
@@ -101,7 +107,7 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
       stpf = dmax(stpmin, stpf);
     }
   } else {
-    if (brackt) {
+    if (uni(brackt)) {
       const double theta = 3.0 * (fp - fy) / (sty - stp) + dy + dp;
       const double s = dmax(dmax(fabs(theta), fabs(dy)), fabs(dp));
       const double ts = theta / s;
@@ -145,7 +151,7 @@ struct Dcsrch {
   // returns false on ERROR (initial derivative not negative)
   __device__ __forceinline__ bool start(double stp, double f, double g) {
 #pragma clang fp contract(off)
-    if (!(g < 0.0)) return false;
+    if (uni(!(g < 0.0))) return false;
     brackt = false;
     stage = 1;
     finit = f;
@@ -173,12 +179,12 @@ struct Dcsrch {
     if (stp == stpmax && f <= ftest && g <= gtest) task = 2;
     if (stp == stpmin && (f > ftest || g >= gtest)) task = 2;
     if (f <= ftest && fabs(g) <= kGtolLs * (-ginit)) task = 1;
-    if (task != 0) return task;
+    if (uni(task != 0)) return task;
     // one dcstep call site on locals (keeps the state in registers): the
     // modified function psi is used in stage 1 when f fell but not enough
     const bool modified = stage == 1 && f <= fx && f > ftest;
     double sx = stx, sy = sty, fxl = fx, gxl = gx, fyl = fy, gyl = gy, fp = f, gp = g;
-    if (modified) {
+    if (uni(modified)) {
       fp = f - stp * gtest;
       fxl = fx - stx * gtest;
       fyl = fy - sty * gtest;
@@ -189,7 +195,7 @@ struct Dcsrch {
     dcstep(sx, fxl, gxl, sy, fyl, gyl, stp, fp, gp, brackt, stmin, stmax);
     stx = sx;
     sty = sy;
-    if (modified) {
+    if (uni(modified)) {
       fx = fxl + stx * gtest;
       fy = fyl + sty * gtest;
       gx = gxl + gtest;
@@ -197,7 +203,7 @@ struct Dcsrch {
     } else {
       fx = fxl; fy = fyl; gx = gxl; gy = gyl;
     }
-    if (brackt) {
+    if (uni(brackt)) {
       if (fabs(sty - stx) >= 0.66 * width1) stp = stx + 0.5 * (sty - stx);
       width1 = width;
       width = fabs(sty - stx);
@@ -269,7 +275,7 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
     // ---- the single evaluation site: f and g at x_eval.  scipy's
     // ScalarFunction memoises the last point: a repeated x costs no
     // evaluation (and no nfev).
-    if (!(have_last && x_eval == x_last)) {
+    if (uni(!(have_last && x_eval == x_last))) {
       if constexpr (ANALYTIC) {
         double f0, g0;
         fg(x_eval, f0, g0);
@@ -278,7 +284,7 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
         g_last = g0;
       } else {
         double h = o.eps;
-        if ((x_eval + h) - x_eval == 0.0)
+        if (uni((x_eval + h) - x_eval == 0.0))
           h = kSqrtEps * (x_eval >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(x_eval));
         if (BOUNDED) {
           const double ld = x_eval - lo, ud = hi - x_eval;
@@ -301,36 +307,36 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
     f = f_last;
     g = g_last;
 
-    if (!in_ls) {
-      if (fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol) return LbfgsResult{x, f, 0, nfev, 0};
+    if (uni(!in_ls)) {
+      if (uni(fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol)) return LbfgsResult{x, f, 0, nfev, 0};
     } else {
       int task = ls.step(stp, f, g * d);
-      if (task == 0) {
+      if (uni(task == 0)) {
         ++ifun;
-        if (ifun - 1 < o.maxls) {
+        if (uni(ifun - 1 < o.maxls)) {
           x_eval = (stp == 1.0) ? z : stp * d + xk;
           continue;
         }
         task = -1;  // iback >= maxls
       }
-      if (task < 0) {
+      if (uni(task < 0)) {
         x = xk; f = fold; g = gold;
-        if (!have_pair) return LbfgsResult{x, f, nit, nfev, 2};
+        if (uni(!have_pair)) return LbfgsResult{x, f, nit, nfev, 2};
         have_pair = false;
         theta = 1.0;
       } else {
         ++nit;
-        if (fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol) return LbfgsResult{x, f, nit, nfev, 0};
-        if ((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))
+        if (uni(fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol)) return LbfgsResult{x, f, nit, nfev, 0};
+        if (uni((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0)))
           return LbfgsResult{x, f, nit, nfev, 1};
-        if (nit >= o.maxiter || nfev > o.maxfun) return LbfgsResult{x, f, nit, nfev, 3};
+        if (uni(nit >= o.maxiter || nfev > o.maxfun)) return LbfgsResult{x, f, nit, nfev, 3};
         const double gd = g * d;
         const double r = g - gold;
         const double rr = r * r;
         double dr, ddum, s;
         if (stp == 1.0) { dr = gd - gdold; ddum = -gdold; s = d; }
         else { dr = (gd - gdold) * stp; s = d * stp; ddum = -gdold * stp; }
-        if (!(dr <= kEpsMch * ddum)) {
+        if (uni(!(dr <= kEpsMch * ddum))) {
           have_pair = true;
           s_last = s;
           y_last = r;
@@ -367,7 +373,7 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
       stp = (nit == 0 && !boxed) ? dmin(1.0 / dnorm, stpmx) : 1.0;
       xk = x; fold = f; gold = g;
       gdold = g * d;
-      if (gdold < 0.0) {
+      if (uni(gdold < 0.0)) {
         ls.stpmax = stpmx;
         ls.start(stp, f, gdold);
         ifun = 1;
@@ -375,7 +381,7 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
         x_eval = (stp == 1.0) ? z : stp * d + xk;
         break;
       }
-      if (!have_pair) return LbfgsResult{x, f, nit, nfev, 2};
+      if (uni(!have_pair)) return LbfgsResult{x, f, nit, nfev, 2};
       have_pair = false;
       theta = 1.0;
     }
