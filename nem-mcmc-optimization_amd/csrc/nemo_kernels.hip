@@ -354,6 +354,25 @@ __global__ void lse_kernel(int rows, int E, int ntiles, const double* __restrict
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double expit_d(double x) { return 1.0 / (1.0 + exp(-x)); }
 
+// One row of exp(T) (TT = double or float) or of the order weights, read
+// through a buffer resource bounded to the row: element q * 64 + lane is the
+// lane's byte offset (one VGPR, fixed) plus a scalar offset, and a read past
+// the row's E elements returns 0 instead of faulting -- no per-element clamp
+// or address arithmetic in the setup of a local optimum.
+struct RowRsrc {
+  __amdgpu_buffer_rsrc_t r;
+  template <typename T>
+  __device__ __forceinline__ RowRsrc(const T* row, int E)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, E * (int)sizeof(T), 0x00020000)) {}
+  template <typename T>
+  __device__ __forceinline__ double at(int lane, int q) const {  // element q * 64 + lane
+    if constexpr (sizeof(T) == 8)
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)lane * 8u, q * 64 * 8, 0));
+    else
+      return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)lane * 4u, q * 64 * 4, 0));
+  }
+};
+
 // c = a / b with a = (lv - 1)*ow_k, b = 1 - s*a + s*(lv - 1)
 // (nem_order_mcmc.py:161-164), operation order kept, no contraction.
 __device__ __forceinline__ double local_c(double lv, double owk, double s) {
@@ -547,15 +566,14 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   LocalObjective<NPL, PROD> obj;
   obj.ltab = ltab;
-  // every lane loads (a clamped index past E) and divides, then padding is
+  // every lane loads (bounded rows: 0 past E) and divides, then padding is
   // selected away: no branch per element, so the 2 NPL loads and the NPL
   // divisions of the setup overlap instead of running one after another
+  const RowRsrc rt(tv, E), ro(owk, E);
 #pragma unroll
   for (int q = 0; q < NPL; ++q) {
-    const int e = q * kWave + lane;
-    const int ec = e < E ? e : E - 1;
-    const double v = local_c((double)tv[ec], owk[ec], s);
-    obj.c[q] = (e < E) ? v : 0.0;  // padding: log(1) = 0
+    const double v = local_c(rt.at<TT>(lane, q), ro.at<double>(lane, q), s);
+    obj.c[q] = (lane < E - q * kWave) ? v : 0.0;  // padding: log(1) = 0
   }
   obj.anc = anc[idx];
 #ifdef NEMO_LO_TRACE
@@ -705,12 +723,12 @@ __global__ __launch_bounds__(NW * kWave) void local_opt_pairs_split_kernel(
   obj.kpost = kpost;
   obj.w = w;
   obj.lane = lane;
+  const RowRsrc rt(tv, E), ro(owk, E);
 #pragma unroll
   for (int q = 0; q < 4 * Obj::L; ++q) {  // (branch-free setup as in local_opt_pairs_kernel)
-    const int e = (4 * Obj::L * w + q) * kWave + lane;
-    const int ec = e < E ? e : E - 1;
-    const double v = local_c((double)tv[ec], owk[ec], s);
-    obj.c[q] = (e < E) ? v : 0.0;  // padding: log(1) = 0
+    const int qq = 4 * Obj::L * w + q;
+    const double v = local_c(rt.at<TT>(lane, qq), ro.at<double>(lane, qq), s);
+    obj.c[q] = (lane < E - qq * kWave) ? v : 0.0;  // padding: log(1) = 0
   }
   obj.anc = anc[idx];
   const LbfgsResult r = lbfgsb1_minimize(obj, s);
