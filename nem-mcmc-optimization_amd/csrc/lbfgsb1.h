@@ -55,7 +55,11 @@ __device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, doub
                               double& dy, double& stp, double fp, double dp, bool& brackt,
                               double stpmin, double stpmax) {
 #pragma clang fp contract(off)
-  const double sgnd = dp * (dx / fabs(dx));
+  // dp * (dx / |dx|) without the division (it heads the case selection's
+  // dependent chain): dx / |dx| is exactly +-1 for a finite non-zero dx, so
+  // the product is +-dp bit for bit; 0 / 0 and inf / inf give NaN, so does
+  // this (and every test of sgnd is then false, as with the quotient)
+  const double sgnd = (dx != 0.0 && fabs(dx) < __builtin_inf()) ? (dx > 0.0 ? dp : -dp) : __builtin_nan("");
   double stpf;
   if (uni(fp > fx)) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
