@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -339,6 +339,15 @@ def main():
     gen = repo_generator()
     if "--only-methods" in sys.argv:
         capture_methods(ref_nem, ref_utils, gen)
+        return
+    if "--only-traj-c3" in sys.argv:
+        # C3 trajectory (the headline model, 64 x 2000): default swap_prob 0.95,
+        # gamma = 2S/E, as the C2 one
+        n_iter = int(sys.argv[sys.argv.index("--only-traj-c3") + 1])
+        net = gen.synthetic_network(64, 2000, 0)
+        mc3 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 64, 2000)
+        order3 = ref_utils.initial_order_guess(mc3.observed_knockdown_mat)
+        capture_traj(ref_mcmc, mc3, order3, 2.0 * 64 / 2000, 0.95, n_iter, f"C3_{n_iter}")
         return
     if "--only-evals" in sys.argv:
         capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)

@@ -242,6 +242,25 @@ def test_trajectory_c2_20():
     assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
 
 
+def test_trajectory_c3_20():
+    """C3, the headline model (64 x 2000): 20 steps of the reference's method()
+    with its seed (tests/golden/make_goldens.py --only-traj-c3 20): identical
+    proposals and accepted moves, every score within 1e-6, the same best order
+    and final random state; the final weights (every step's 2016 local optima
+    carried into the next) within the forward-difference noise."""
+    z = golden("traj_C3_20.npz")
+    m = generator.synthetic_nem(64, 2000, 0)
+    state = random.getstate()
+    smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
+                             int(z["n_iter"]), state)
+    assert np.array_equal(np.array(smp.accepted), z["acc"])
+    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
+    assert abs(best - float(z["best_score"])) <= LL_TOL
+    assert np.array_equal(smp.best_order, z["best_order"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    assert np.array_equal(smp.parent_weights > 0.5, z["final_W"] > 0.5)
+
+
 def test_edge_cases():
     # smallest model, E not a multiple of the 64-effect tile, E = 1
     for s, e in ((2, 1), (3, 65), (5, 130)):
