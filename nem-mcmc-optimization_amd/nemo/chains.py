@@ -475,7 +475,7 @@ def gather_best(best_scores, best_orders, device=None):
 
 
 def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_steps: int = 2, inv_workers=None,
-           device=None, cap: int = 0):
+           device=None, cap: int = 0, repeats: int = 1):
     """BASELINE config C4 on the default process group (or alone without one):
     ``n_chains`` independent chains of ``nem`` sharded over the ranks
     (``shard``; chain c keeps seed 1234 + c and the reference's initial order
@@ -486,8 +486,10 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
     ranks run ``warmup_steps`` untimed steps on a throw-away batch first.
 
     Returns, on every rank, a dict: wall seconds of the timed run (max over
-    ranks, barrier before), chain-steps/s, the gathered scores and orders and
-    the global best."""
+    ranks, barrier before; with ``repeats`` > 1 the run is repeated from the
+    same seeds -- the same results -- and the median of the runs' walls is
+    reported, the host side being noisy run to run), chain-steps/s, the
+    gathered scores and orders and the global best."""
     import hashlib
     import time
 
@@ -510,30 +512,35 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
         if warmup_steps > 0 and len(mine):
             ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
                        inv_pool=pool).run(warmup_steps)
-        cb = ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
-                        inv_pool=pool) if len(mine) else None
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        if cb is not None:
-            best, orders = cb.run(steps)
-        else:
-            best, orders = np.zeros(0), np.zeros((0, nem.num_s), dtype=np.int32)
-        if world > 1:
-            all_s, all_o = gather_best(best, orders, device=device)
-        else:
-            all_s, all_o = np.asarray(best, dtype=np.float64), np.asarray(orders)
-        wall = time.perf_counter() - t0
+        walls = []
+        for _ in range(max(1, int(repeats))):
+            cb = ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
+                            inv_pool=pool) if len(mine) else None
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            if cb is not None:
+                best, orders = cb.run(steps)
+            else:
+                best, orders = np.zeros(0), np.zeros((0, nem.num_s), dtype=np.int32)
+            if world > 1:
+                all_s, all_o = gather_best(best, orders, device=device)
+            else:
+                all_s, all_o = np.asarray(best, dtype=np.float64), np.asarray(orders)
+            wall = time.perf_counter() - t0
+            if world > 1:
+                import torch
+                t = torch.tensor([wall], dtype=torch.float64, device=device if device is not None else "cpu")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                wall = float(t.item())
+            walls.append(wall)
     finally:
         if pool is not None:
             pool.close()
-    if world > 1:
-        import torch
-        t = torch.tensor([wall], dtype=torch.float64, device=device if device is not None else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = float(np.median(walls))
     g = int(np.argmax(all_s))
     return {"wall_s": wall, "chain_steps_per_s": n_chains * steps / wall, "ms_per_step": 1e3 * wall / steps,
+            "ms_per_step_runs": [1e3 * w / steps for w in walls],
             "n_ranks": world, "chains_per_rank": len(mine), "inv_workers_per_rank": nw if pool else 0,
             "n_gathered": int(len(all_s)), "best_score": float(all_s[g]), "best_chain": g,
             "best_order": [int(v) for v in all_o[g]],
