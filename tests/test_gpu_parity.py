@@ -242,23 +242,32 @@ def test_trajectory_c2_20():
     assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
 
 
-def test_trajectory_c3_20():
-    """C3, the headline model (64 x 2000): 20 steps of the reference's method()
-    with its seed (tests/golden/make_goldens.py --only-traj-c3 20): identical
-    proposals and accepted moves, every score within 1e-6, the same best order
-    and final random state; the final weights (every step's 2016 local optima
-    carried into the next) within the forward-difference noise."""
-    z = golden("traj_C3_20.npz")
+# steps whose score may leave 1e-6 of the reference's: at C3 a few of each
+# step's 2016 local optima land within the forward-difference noise (h = 1e-8)
+# of scipy's, and a weight that sits at 0.5 can binarise to the other side
+# (DESIGN.md 3.5); over the 100-step run that happens once (step 27, then the
+# chains re-align: the accepted moves, best order and random state stay equal)
+@pytest.mark.parametrize("n,max_off", [(20, 0), (100, 1)])
+def test_trajectory_c3(n, max_off):
+    """C3, the headline model (64 x 2000): n steps of the reference's method()
+    with its seed (tests/golden/make_goldens.py --only-traj-c3 n): identical
+    proposals and accepted moves, scores within 1e-6 (all but max_off steps),
+    the same best score and order, the same final random state, and final
+    weights (every step's 2016 local optima carried into the next) within the
+    forward-difference noise and binarised the same."""
+    z = golden(f"traj_C3_{n}.npz")
     m = generator.synthetic_nem(64, 2000, 0)
     state = random.getstate()
     smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
                              int(z["n_iter"]), state)
     assert np.array_equal(np.array(smp.accepted), z["acc"])
-    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
+    d = np.abs(np.array(smp.all_score_list) - z["all_scores"])
+    assert int((d > LL_TOL).sum()) <= max_off, np.where(d > LL_TOL)[0].tolist()
     assert abs(best - float(z["best_score"])) <= LL_TOL
     assert np.array_equal(smp.best_order, z["best_order"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
     assert np.array_equal(smp.parent_weights > 0.5, z["final_W"] > 0.5)
+    assert np.max(np.abs(smp.parent_weights - z["final_W"])) <= 1e-4
 
 
 def test_edge_cases():
