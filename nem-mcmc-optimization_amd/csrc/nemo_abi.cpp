@@ -469,6 +469,40 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
   const size_t S = c.S, E = c.E;
   hipStream_t st = c.stream;
+  if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.step_host_sum && batch <= 64) {
+    // ll only (one sampler's calculate_ll): the fused step's transfer pattern --
+    // pos and W staged in the pinned slot 0 and sent in ONE copy, the kernel's
+    // per-evaluation partials (or its own sums) back in ONE copy, summed on the
+    // host in the device's fixed order (sum_partials_host: the same bits as the
+    // finalize launch this saves); pageable copies cost ~10 us each
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t n = batch, npart = (size_t)nemo::factored_partials(c);
+    const size_t o_w01 = up(n * S * 4), o_part = o_w01 + up(n * S * S * 8), o_ll = o_part + up(n * npart * 8);
+    const size_t total = o_ll + up(n * 8);
+    if ((rc = step_stage(c, 0, total))) return rc;
+    char* hs = (char*)c.h_stage[0];
+    char* ds = (char*)c.d_step[0];
+    memcpy(hs, pos, n * S * 4);
+    memcpy(hs + o_w01, w01, n * S * S * 8);
+    HIPCHK(hipMemcpyAsync(ds, hs, o_part, hipMemcpyHostToDevice, st));
+    int np = 0;
+    c.part_out = (double*)(ds + o_part);
+    const hipError_t e = nemo::launch_score_factored(c, batch, cap, (const int32_t*)ds, (const double*)(ds + o_w01),
+                                                     (double*)(ds + o_ll), nullptr, nullptr, nullptr, st, false, &np);
+    c.part_out = nullptr;
+    HIPCHK(e);
+    if ((size_t)np > npart) return fail(NEMO_ERR_STATE, "score partials exceed the slot");
+    HIPCHK(hipMemcpyAsync(hs + o_part, ds + o_part, total - o_part, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (np > 0) {
+      const double* part = (const double*)(hs + o_part);
+      for (size_t b = 0; b < n; ++b) ll_out[b] = nemo::host::sum_partials_host(part + b * (size_t)np, np);
+    } else {
+      memcpy(ll_out, hs + o_ll, n * 8);
+    }
+    c.ow_chains = 0;
+    return NEMO_OK;
+  }
   double* d_cells = nullptr;
   if (cells_out) HIPCHK(hipMallocAsync((void**)&d_cells, batch * (S + 1) * E * 8, st));
   HIPCHK(hipMemcpyAsync(c.d_pos, pos, batch * S * 4, hipMemcpyHostToDevice, st));

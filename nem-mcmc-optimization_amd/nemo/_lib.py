@@ -41,7 +41,7 @@ SIGNATURES = [
     ("nemo_reserve", C.c_int, [_vp, C.c_int, C.c_int]),
     ("nemo_stage_tables", C.c_int, [_vp, _f64p, _f64p]),
     ("nemo_stage_knockdown", C.c_int, [_vp, _u8p, C.c_double, C.c_double]),
-    ("nemo_score", C.c_int, [_vp, C.c_int, _i32p, _f64p, C.c_int, _f64p, _f64p, _f64p, _f64p]),
+    ("nemo_score", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp]),  # addr()
     ("nemo_score_dev", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("nemo_score_group_dev", C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int, _vp, _vp]),
     ("nemo_lse", C.c_int, [_vp, C.c_int, _f64p, _f64p, _f64p, _f64p]),

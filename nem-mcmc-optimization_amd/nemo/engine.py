@@ -110,8 +110,10 @@ class Engine:
         cs = np.empty((b, self.E)) if want_cs else None
         cells = np.empty((b, self.S + 1, self.E)) if want_cells else None
         ow = np.empty((b, self.S + 1, self.E)) if want_ow else None
-        check(_lib.load().nemo_score(self._ctx, b, ptr(pos, _lib._i32p), ptr(w01), int(cap), ptr(ll),
-                                     ptr(cs), ptr(cells), ptr(ow)))
+        a = _lib.addr  # plain addresses (~0.4 us each against ~4 for ctypes.data_as)
+        check(_lib.load().nemo_score(self._ctx, b, a(pos), a(w01), int(cap), a(ll),
+                                     None if cs is None else a(cs), None if cells is None else a(cells),
+                                     None if ow is None else a(ow)))
         if not (want_cs or want_cells or want_ow):
             return ll
         return {"ll": ll, "cs": cs, "cells": cells, "ow": ow}
