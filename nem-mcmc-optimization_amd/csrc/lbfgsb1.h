@@ -234,6 +234,15 @@ __device__ __forceinline__ double projg(double x, double g, bool has_lo, double 
   return has_lo ? dmin(x - lo, g) : g;
 }
 
+#ifdef NEMO_LO_TRACE
+// cycle probe (instrumented builds only): the line-search step's share,
+// accumulated into objectives that carry a cy_ls counter
+template <class F>
+__device__ __forceinline__ auto trace_ls(F& f, long long c, int) -> decltype(f.cy_ls += c, void()) { f.cy_ls += c; }
+template <class F>
+__device__ __forceinline__ void trace_ls(F&, long long, long) {}
+#endif
+
 }  // namespace lb
 
 // Options of the bounded / analytic-gradient variant (the fixed-order
@@ -314,7 +323,14 @@ __device__ __forceinline__ LbfgsResult lbfgsb1_minimize_opts(FG& fg, double x0, 
     if (uni(!in_ls)) {
       if (uni(fabs(lb::projg<BOUNDED>(x, g, has_lo, lo, has_hi, hi)) <= o.gtol)) return LbfgsResult{x, f, 0, nfev, 0};
     } else {
+#ifdef NEMO_LO_TRACE
+      const long long tl0 = clock64();
+#endif
       int task = ls.step(stp, f, g * d);
+#ifdef NEMO_LO_TRACE
+      { const double keep = stp; asm volatile("" :: "v"(keep)); }
+      lb::trace_ls(fg, clock64() - tl0, 0);
+#endif
       if (uni(task == 0)) {
         ++ifun;
         if (uni(ifun - 1 < o.maxls)) {

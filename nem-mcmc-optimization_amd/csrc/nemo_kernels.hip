@@ -398,7 +398,7 @@ struct LocalObjective {
   // needing at least that many f-evaluations, the cycles of its minimisation
   // and of the objective's parts (expit, products, log + wave sums); run
   // tools/lo_stats.py with NEMO_LIBRARY pointing at that build
-  mutable long long cy_exp = 0, cy_prod = 0, cy_tail = 0, cy_calls = 0;
+  mutable long long cy_exp = 0, cy_prod = 0, cy_tail = 0, cy_calls = 0, cy_ls = 0;
 #endif
   __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
 #pragma clang fp contract(off)
@@ -583,8 +583,8 @@ __global__ __launch_bounds__(256, kLocalOptWavesPerSimd) void local_opt_pairs_ke
 #ifdef NEMO_LO_TRACE
   const long long tend = clock64();
   if (lane == 0 && r.nfev >= NEMO_LO_TRACE)
-    printf("lo_trace b %d i %d k %d nfev %d nit %d min %lld calls %lld exp %lld prod %lld tail %lld\n", b, i, k,
-           r.nfev, r.nit, tend - ts, obj.cy_calls, obj.cy_exp, obj.cy_prod, obj.cy_tail);
+    printf("lo_trace b %d i %d k %d nfev %d nit %d min %lld calls %lld exp %lld prod %lld tail %lld ls %lld\n", b, i,
+           k, r.nfev, r.nit, tend - ts, obj.cy_calls, obj.cy_exp, obj.cy_prod, obj.cy_tail, obj.cy_ls);
 #endif
   if (lane == 0) {
     const double wx = expit_d(r.x);
