@@ -49,10 +49,34 @@ def algorithmic_bytes_per_eval(S, E, cap, b):
     return n_pairs(S, cap) * E * b + (S + 1) * E * b + S * S * b + 4 * S + b
 
 
+def factored_bytes_per_launch(S, E, B):
+    """Algorithmic HBM bytes of one launch of the factored kernels (DESIGN.md
+    3.1, 5): what they must read and write at least -- per evaluation its
+    weights (S^2 f64), order (S int32) and ll (f64), and once per launch the
+    model: U ((S+1) x E f64) and the D1 bit rows (S x ceil(E/64) u64).  They
+    never read the S x S x E table T, so SURVEY.md 8(d)'s T-streaming bytes
+    do not describe them (that model prices the streaming kernel)."""
+    return B * (S * S * 8 + 4 * S + 8) + (S + 1) * E * 8 + S * ((E + 63) // 64) * 8
+
+
 def algorithmic_flops_per_eval(S, E, cap):
     """Factored form: cell = U + G + Delta.D1 over the permissible (i, j):
     2 FLOP per (pair, effect)."""
     return 2 * n_pairs(S, cap) * E
+
+
+def host_cpu():
+    """The host CPU's model name (/proc/cpuinfo): the same oracle loop runs
+    ~2x faster on the GPU box's host than in the build container (SURVEY.md
+    6 was measured there), so every CPU figure names its CPU."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(m, seconds=10.0, config="C3"):
@@ -175,7 +199,11 @@ def stream_roofline(B, bpe, kern_ms, tr):
 
 
 def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, world, dist,
-                warmup_s=0.0):
+                warmup_s=0.0, collective=None):
+    """``collective``: run the barriers and the best-score all-gather on the
+    default process group (default: world > 1; rank-0-only extras pass
+    world = 1 and run none)."""
+    coll = world > 1 if collective is None else collective
     def step():
         eng.score_dev(B, d_pos.data_ptr(), d_w01.data_ptr(), d_ll.data_ptr(), cap=cap, stream=stream)
 
@@ -191,7 +219,7 @@ def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, w
         for _ in range(10):
             step()
         torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     # kernel time = HIP events recorded on the launch stream around the K
@@ -207,15 +235,15 @@ def timed_steps(eng, torch, B, cap, steps, warmup, d_pos, d_w01, d_ll, stream, w
     for _ in range(steps):
         step()
     ev1.record(ts)
-    if world > 1:
+    if coll:
         # C4: gather every rank's per-chain best score (tiny, latency-bound)
         best = d_ll.max().reshape(1)
         if dist.get_backend() != "nccl":
             best = best.cpu()
-        allb = [torch.empty_like(best) for _ in range(world)]
+        allb = [torch.empty_like(best) for _ in range(dist.get_world_size())]
         dist.all_gather(allb, best)
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -294,6 +322,7 @@ KERNEL_NAMES = {
     "factored": "score_factored_kernel (fp64 MFMA 16x16x4 + fused log-sum-exp)",
     "pipe": "score_factored_pipe_kernel (fp64 MFMA 16x16x4, U as the C-init, fused log-sum-exp)",
     "win2": "score_window2_kernel (capped lookup tables walked from registers)",
+    "win": "score_window_kernel (capped lookup tables, round-1 form: row bits re-read from LDS)",
 }
 ARITH = {
     "i8l": "int8 fixed point 2^-38/ln2 + fp64 LSE",
@@ -307,7 +336,7 @@ def kernel_tag(fk):
     """profiles/*.json key tag of the kernel fact_kernel ``fk`` launches."""
     if fk in (18, 19):
         return "i8w"
-    if fk in (10, 11, 12, 14, 16, 17):
+    if fk in (10, 11, 12, 14, 16, 17, 20):
         return "i8l"
     if fk == 13:
         return "i8s"
@@ -315,8 +344,10 @@ def kernel_tag(fk):
         return "i8o"
     if fk in (4, 5, 6):
         return "i8"
-    if fk in (9,):
+    if fk == 9:
         return "win2"
+    if fk == 15:
+        return "win"
     if fk in (2, 3):
         return "pipe"
     return "factored"
@@ -342,10 +373,19 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
         a = B * ops / kern_s / 1e12
         secondary["int8_mfma"] = {"achieved": a, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                                   "frac": a / I8_MFMA_PEAK_TOPS, "ops_per_eval": ops}
+    fbytes = factored_bytes_per_launch(S, E, B)
+    hbm_alg = fbytes / kern_s / 1e9
+    secondary["hbm"] = {"algorithmic_bytes_per_launch": fbytes, "achieved": hbm_alg, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS,
+                        "note": "algorithmic bytes of the factored form (weights, orders and lls of the batch + "
+                                "U and the D1 bits once; bench.factored_bytes_per_launch) / this run's launch time"}
     if traffic:
         hbm = traffic["bytes_per_launch"] / kern_s / 1e9
-        secondary["hbm"] = {"achieved": hbm, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm / HBM_PEAK_GBS,
-                            "note": "PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) / this run's launch time"}
+        secondary["hbm"].update({"pmc_bytes_per_launch": traffic["bytes_per_launch"], "pmc_achieved": hbm,
+                                 "pmc_frac": hbm / HBM_PEAK_GBS,
+                                 "pmc_over_algorithmic": traffic["bytes_per_launch"] / fbytes,
+                                 "pmc_note": "PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, this build) / "
+                                             "this run's launch time"})
     if valu and "SQ_LDS_IDX_ACTIVE" in valu:
         lds = valu["SQ_LDS_IDX_ACTIVE"] / kern_s / 1e12
         peak = 256 * CLOCK_MAX_GHZ / 1e3
@@ -383,6 +423,34 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
                     "how far the int8 fixed-point reformulation is past an fp64 matrix-core roofline; not a "
                     "hardware fraction"}
     return roof
+
+
+def c3_fp64(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, ll_ref, steps=10, warmup_s=0.3):
+    """The headline workload (same model, same resident inputs, same B) in
+    fp64 arithmetic: the fp64 MFMA factored kernels (fact_kernel 2: pipelined,
+    U as the C-init; 1: chunked), priced against the fp64 matrix-core peak
+    (2*P*E FLOP of the contraction per evaluation), next to the fixed-point
+    headline kernel's lls."""
+    fk0 = eng.get_option("fact_kernel")
+    d_ll = torch.zeros(B, dtype=torch.float64, device="cuda")
+    out = {"workload": f"C3: S={S} E={E}, {B} evaluations per launch, fp64 arithmetic throughout"}
+    try:
+        for name, fk in (("f64_mfma_pipelined_kernel", 2), ("f64_mfma_chunked_kernel", 1)):
+            eng.set_option("fact_kernel", fk)
+            wall, kms, _ = timed_steps(eng, torch, B, cap, steps, 2, d_pos, d_w01, d_ll, stream, 1, dist,
+                                       warmup_s=warmup_s)
+            fl = B * algorithmic_flops_per_eval(S, E, cap) / (kms / 1e3) / 1e12
+            out[name] = {"fact_kernel": fk, "evals_per_s": B * steps / wall, "kernel_avg_ms": kms,
+                         "roofline": {"bound": "mfma", "achieved": fl, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                                      "frac": fl / F64_MFMA_PEAK_TF,
+                                      "flops_per_eval": algorithmic_flops_per_eval(S, E, cap)},
+                         "max_abs_ll_diff_vs_headline": float(np.max(np.abs(d_ll.cpu().numpy() - ll_ref)))}
+    finally:
+        eng.set_option("fact_kernel", fk0)
+    best = max((k for k in out if k.endswith("_kernel")), key=lambda k: out[k]["evals_per_s"])
+    out["best"] = best
+    out["evals_per_s"] = out[best]["evals_per_s"]
+    return out
 
 
 def wide_uncapped(torch, dist, stream, batch=2048, steps=5, warmup_s=0.3):
@@ -505,6 +573,7 @@ def main():
                         "step per MCMC step per rank), one all-gather of (best score, best order)",
             "collective": (f"all_gather over {'RCCL' if backend == 'nccl' else backend}"
                            if world > 1 else None),
+            "accepted": None,
             "reference_cpu_s_per_chain_step": 1.2}
 
     if rank == 0 and not args.no_extras:
@@ -519,6 +588,10 @@ def main():
             "evals_per_s": Bs * 10 / w_s, "batch": Bs, "kernel_avg_ms": k_s,
             "roofline": stream_roofline(Bs, bpe, k_s, tr)}
         eng.set_option("score_path", PATHS[args.path])
+        if factored and args.config in ("C3", "C2"):
+            # the same workload in fp64 arithmetic (the headline's dtype is fixed point)
+            extras["c3_fp64"] = c3_fp64(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, ll,
+                                        warmup_s=min(args.warmup_seconds, 0.3))
         # fused per-step scorer of the sampler: 16 chains (C4 share of one GPU)
         from nemo.nem_order_mcmc import SIG0, SIG1
         nch = 16
@@ -637,8 +710,11 @@ def main():
         rec.update(extras)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(m, args.cpu_seconds, args.config)
+            rec["cpu_baseline"]["host_nproc"] = os.cpu_count()
+            rec["cpu_baseline"]["host_cpu"] = host_cpu()
             if args.cpu_procs > 1:  # also all the host cores the round budget allows
                 rec["cpu_baseline_procs"] = cpu_baseline_procs(args.config, args.cpu_procs, args.cpu_seconds)
+                rec["cpu_baseline_procs"]["host_nproc"] = os.cpu_count()
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

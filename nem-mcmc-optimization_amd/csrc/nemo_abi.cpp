@@ -490,8 +490,7 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
     const hipError_t e = nemo::launch_score_factored(c, batch, cap, (const int32_t*)ds, (const double*)(ds + o_w01),
                                                      (double*)(ds + o_ll), nullptr, nullptr, nullptr, st, false, &np);
     c.part_out = nullptr;
-    HIPCHK(e);
-    if ((size_t)np > npart) return fail(NEMO_ERR_STATE, "score partials exceed the slot");
+    HIPCHK(e);  // np <= npart: launch_score_factored checks score_partials before launching
     HIPCHK(hipMemcpyAsync(hs + o_part, ds + o_part, total - o_part, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (np > 0) {
@@ -762,12 +761,12 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
                                     (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st,
                                     c.step_host_sum && L.o_part < L.total ? (double*)(ds + L.o_part) : nullptr,
                                     &np2);
-    if (r) return r;
-    if ((size_t)np2 * n * 8 > L.total - L.o_part) return fail(NEMO_ERR_STATE, "eval #2 partials exceed the slot");
+    if (r) return r;  // np2 <= step_npart: checked by launch_score_factored before it launched
     HIPCHK(hipMemcpyAsync(hs + L.o_wn, ds + L.o_wn, L.total - L.o_wn, hipMemcpyDeviceToHost, st));
     return NEMO_OK;
   };
   Ctx::StepGraph* sg = nullptr;
+  bool graphs_off = false;  // the capture failed: decided after the direct launch below
   if (c.graphs && !c.timing) {
     for (auto& g : c.step_graph)
       if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.slot == slot &&
@@ -777,6 +776,9 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
       Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
       c.step_graph_next = (c.step_graph_next + 1) % Ctx::kStepGraphs;
       if (g.exec) {
+        // the evicted exec may be the one the other staging slot launched and
+        // is still running: every step runs on st, so draining it is enough
+        HIPCHK(hipStreamSynchronize(st));
         (void)hipGraphExecDestroy(g.exec);
         g.exec = nullptr;
       }
@@ -784,6 +786,13 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
       if (hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess) {
         const int r = enqueue();
         const hipError_t ee = hipStreamEndCapture(st, &graph);
+        if (r != NEMO_OK && r != NEMO_ERR_HIP) {
+          // a call error (argument, state, unsupported kernel): the caller's,
+          // not the capture's -- graphs stay on
+          if (graph) (void)hipGraphDestroy(graph);
+          (void)hipGetLastError();
+          return r;
+        }
         if (r == NEMO_OK && ee == hipSuccess && graph &&
             hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0) == hipSuccess) {
           g.nchains = nchains;
@@ -796,12 +805,12 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
           sg = &g;
         } else {
           g.exec = nullptr;
-          c.graphs = 0;  // this runtime does not capture the step: launch it directly from now on
+          graphs_off = true;
         }
         if (graph) (void)hipGraphDestroy(graph);
         (void)hipGetLastError();
       } else {
-        c.graphs = 0;
+        graphs_off = true;
       }
     }
   }
@@ -810,8 +819,11 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
     c.ow_chains = nchains;  // nemo_optimal_weights_dev's host-side effect
     np2 = sg->np2;
   } else if ((rc = enqueue())) {
-    return rc;
+    return rc;  // the direct launch fails as well: the call's error, graphs stay on
   }
+  // the step ran without the graph the capture could not make: this runtime
+  // does not capture it, so launch directly from now on
+  if (graphs_off) c.graphs = 0;
   c.step_np2[slot] = np2;
   HIPCHK(hipEventRecord(c.step_done[slot], st));
   return NEMO_OK;

@@ -571,6 +571,19 @@ int factored_partials(const Ctx& c) {
   return std::max(n, (c.E + 63) / 64);  // the lookup-table kernel: one per word
 }
 
+int score_partials(const Ctx& c, int fk) {
+  const int nt = (c.E + 15) / 16;
+  if (fk == 9 || fk == 15) return c.nwords;                        // launch_score_window
+  if (fk == 18 || fk == 19) return (nt + kWideSetT - 1) / kWideSetT;  // launch_i8w_t
+  if (fk >= 4) return (nt + 7) / 8;                                 // launch_i8_t / i8o_t / i8l_t / i8s / i8p
+  if (fk == 2 || fk == 3) {                                         // launch_pipe_t
+    const int wv = fk == 3 ? 8 : 4, tpb = kPipeTilesPerWave * wv;
+    return ((nt + tpb - 1) / tpb) * wv;
+  }
+  const int cols = kFactWaves * 16;                                 // launch_fact_w
+  return ((c.E + cols - 1) / cols) * kFactWaves;
+}
+
 int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound) {
   if (bound) *bound = 0.0;
   if (!c.factored) return -1;
@@ -631,6 +644,10 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   // tiles per iteration; 20: 10 as a prep-only and a walk-only launch)
   const int fk = resolve_fact_kernel(c, cap, ll_only, nullptr);
   if (fk < 0) return hipErrorInvalidValue;  // asked for a kernel the staged model does not support
+  // every partial buffer (d_fpartial, a redirected part_out) holds
+  // factored_partials per evaluation: checked before anything is launched
+  const int np_pred = score_partials(c, fk);
+  if (np_pred > factored_partials(c)) return hipErrorInvalidValue;
   const bool is_auto = c.fact_kernel == 0;
   const bool win = fk == 9 || fk == 15;
   const bool wide = fk == 18 || fk == 19;
@@ -694,6 +711,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
     }
   }
   if (err != hipSuccess) return err;
+  if (np != np_pred) return hipErrorUnknown;  // score_partials out of step with a launcher: a build bug
   if (e1) {
     (void)hipEventRecord(e1, st);
     c.launches++;

@@ -1744,7 +1744,7 @@ hipError_t launch_i8l_t(Ctx& c, int batch, int cap, const int32_t* d_pos, const 
 // not depend on the batch size (one block per evaluation, in-kernel sum).
 // ---------------------------------------------------------------------------
 constexpr int kWideKH = 2;    // K halves
-constexpr int kWideSetT = 2;  // tiles per partial
+// kWideSetT (nemo_internal.h): tiles per partial
 
 // i8l_digits into the two-half layout: slice sl, half j >> 6
 __device__ __forceinline__ void i8w_digits(int8_t* A8, int i, int j, double d) {

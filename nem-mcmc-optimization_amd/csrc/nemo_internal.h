@@ -221,6 +221,12 @@ int pairs_per_chain(int S, int cap);
 // factored MFMA path (nemo_factored.hip)
 int factored_spad(int S);
 int factored_partials(const Ctx& c);
+// the partials per evaluation the kernel fact_kernel `fk` (resolved) writes:
+// each launcher's own formula, known before anything is launched, so a
+// caller that redirects them (Ctx::part_out) checks its buffer first
+int score_partials(const Ctx& c, int fk);
+// 16-effect tiles per partial of score_i8w_kernel
+constexpr int kWideSetT = 2;
 // int8 matrix-core factored path (nemo_factored_i8.hip), S <= 64, ll only:
 // one kernel (digits of Delta built in LDS + score); partials per 8-tile set
 // (*finalized: ll already written -- one block per evaluation -- else the

@@ -496,10 +496,11 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
     from . import utils
     from .invpool import InvPool, default_workers
 
-    world, rank = 1, 0
+    world, rank, pg = 1, 0, False
     try:
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized():
+        pg = dist.is_available() and dist.is_initialized()
+        if pg:
             world, rank = dist.get_world_size(), dist.get_rank()
     except ImportError:
         dist = None
@@ -516,19 +517,19 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
         for _ in range(max(1, int(repeats))):
             cb = ChainBatch(nem, [order] * len(mine), seeds=seeds, engine=engine, on_fail="continue", cap=cap,
                             inv_pool=pool) if len(mine) else None
-            if world > 1:
+            if pg:
                 dist.barrier()
             t0 = time.perf_counter()
             if cb is not None:
                 best, orders = cb.run(steps)
             else:
                 best, orders = np.zeros(0), np.zeros((0, nem.num_s), dtype=np.int32)
-            if world > 1:
+            if pg:  # a process group (even of one rank): the collective runs
                 all_s, all_o = gather_best(best, orders, device=device)
             else:
                 all_s, all_o = np.asarray(best, dtype=np.float64), np.asarray(orders)
             wall = time.perf_counter() - t0
-            if world > 1:
+            if pg:
                 import torch
                 t = torch.tensor([wall], dtype=torch.float64, device=device if device is not None else "cpu")
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -543,6 +544,8 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
             "ms_per_step_runs": [1e3 * w / steps for w in walls],
             "n_ranks": world, "chains_per_rank": len(mine), "inv_workers_per_rank": nw if pool else 0,
             "n_gathered": int(len(all_s)), "best_score": float(all_s[g]), "best_chain": g,
+            "gathered_over": dist.get_backend() if pg else None,
+            "accepted": None if cb is None else cb.accepted,
             "best_order": [int(v) for v in all_o[g]],
             "scores_sha256": hashlib.sha256(np.ascontiguousarray(all_s, dtype=np.float64).tobytes()).hexdigest()[:16],
             "scores": all_s, "orders": all_o}

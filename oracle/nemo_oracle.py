@@ -315,9 +315,17 @@ class OracleSampler:
         perm[i], perm[j] = perm[j], perm[i]
         return perm, i1, i2
 
-    # nem_order_mcmc.py:257-310 with opt_weights as pass-through
+    def dag_score(self):
+        """The documented ``opt_weights`` pass-through: the
+        score of create_dag's binarised weights -- create_dag even when the
+        step used create_nem."""
+        return calculate_ll(cell_ratios(self.u, self.t, self.parents, self._mapped(self.dag_weights(self.w))))[1]
+
+    # nem_order_mcmc.py:257-310 with opt_weights as pass-through (:258-259:
+    # the first step's score is replaced by the pass-through's)
     def method(self, swap_prob=0.95, gamma=1, n_iterations=500, use_nem=False):
-        curr = self.optimal_weights(use_nem=use_nem)
+        self.optimal_weights(use_nem=use_nem)
+        curr = self.dag_score()
         best = curr
         curr_perm = self.perm_order
         best_order = curr_perm

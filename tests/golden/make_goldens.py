@@ -7,7 +7,7 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N | --only-traj-nem]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -130,9 +130,11 @@ def capture_evals(ref_nem, ref_mcmc, ref_utils, gen, name, s, e, seed, cap, n_ev
     print(f"eval_{name}: S={s} E={e} cap={cap} ll={lls}")
 
 
-def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_local_every=0):
+def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_local_every=0, use_nem=False):
     """Run the patched reference sampler, recording every proposal and
-    decision (and a sample of local optimisations)."""
+    decision (and a sample of local optimisations).  ``use_nem``: the
+    transitive-closure DAG path of method() (nem_order_mcmc.py:203-204,
+    283-284; utils.py:37-54)."""
     rec = {"perm": [], "i1": [], "i2": [], "acc": []}
     local = []
     cls = ref_mcmc.NEMOrderMCMC
@@ -173,7 +175,7 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
     cls.get_new_order, cls.accepting, cls.calculate_local_optimum = new_order, accepting, local_opt
     try:
         mc = cls(m, order)
-        best, _dag = quiet(mc.method, n_iterations=n_iter, gamma=gamma, swap_prob=swap_prob)
+        best, best_dag = quiet(mc.method, n_iterations=n_iter, gamma=gamma, swap_prob=swap_prob, use_nem=use_nem)
     finally:
         cls.get_new_order, cls.accepting, cls.calculate_local_optimum = orig_new, orig_acc, orig_loc
     out = dict(order0=np.asarray(order), gamma=gamma, swap_prob=swap_prob, n_iter=n_iter,
@@ -181,6 +183,7 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
                acc=np.array(rec["acc"]), all_scores=np.array(mc.all_score_list),
                curr_scores=np.array(mc.curr_score_list), best_scores=np.array(mc.best_score_list),
                best_score=best, best_order=np.asarray(mc.best_order), final_W=mc.parent_weights,
+               best_dag=np.asarray(best_dag), use_nem=use_nem,
                rng_state_after=np.array(random.getstate()[1], dtype=np.int64))
     np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), **out)
     print(f"traj_{name}: best={best} accepts={int(np.sum(rec['acc']))}")
@@ -348,6 +351,14 @@ def main():
         mc3 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 64, 2000)
         order3 = ref_utils.initial_order_guess(mc3.observed_knockdown_mat)
         capture_traj(ref_mcmc, mc3, order3, 2.0 * 64 / 2000, 0.95, n_iter, f"C3_{n_iter}")
+        return
+    if "--only-traj-nem" in sys.argv:
+        # C1's model and stream (net2, full constructor, post-NEM state as in
+        # main()), method(use_nem=True), main.py's swap_prob 0.90 and gamma 2S/E
+        adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
+        m = quiet(ref_nem.NEM, adj, end, err, s, e)
+        order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+        capture_traj(ref_mcmc, m, order, 2.0 * s / e, 0.90, 50, "net2_nem_50", use_nem=True)
         return
     if "--only-evals" in sys.argv:
         capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)

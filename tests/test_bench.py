@@ -78,6 +78,10 @@ def test_roofline_is_a_hardware_fraction(monkeypatch):
 def test_kernel_tags():
     assert bench.kernel_tag(10) == "i8l" and bench.kernel_tag(8) == "i8o" and bench.kernel_tag(4) == "i8"
     assert bench.kernel_tag(9) == "win2" and bench.kernel_tag(2) == "pipe" and bench.kernel_tag(1) == "factored"
+    # fact_kernel 20 is score_i8l_kernel split into a prep-only and a walk-only
+    # launch; 15 is the capped lookup-table kernel's round-1 form
+    assert bench.kernel_tag(20) == "i8l" and bench.kernel_tag(15) == "win" and bench.kernel_tag(13) == "i8s"
+    assert bench.kernel_tag(18) == "i8w" and bench.kernel_tag(3) == "pipe"
 
 
 @pytest.mark.timeout(180)

@@ -232,6 +232,30 @@ def test_trajectory_net2_200(net2):
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
 
 
+def test_trajectory_net2_use_nem_50(net2):
+    """method(use_nem=True): the transitive-closure DAG scores eval #2 and
+    the accept step (nem_order_mcmc.py:203-204, 283-284; utils.py:37-54).
+    50 steps on network2 with the reference's seed (make_goldens.py
+    --only-traj-nem): identical proposals and accepted moves, scores within
+    1e-6, the same best score, order and (closure) DAG, the same random
+    state after the run."""
+    m, state = net2
+    z = golden("traj_net2_nem_50.npz")
+    assert bool(z["use_nem"])
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    random.setstate(state)
+    smp = NEMOrderMCMC(m, z["order0"])
+    best, best_dag = smp.method(n_iterations=int(z["n_iter"]), gamma=float(z["gamma"]),
+                                swap_prob=float(z["swap_prob"]), verbose=False, use_nem=True)
+    assert np.array_equal(np.array(smp.accepted), z["acc"])
+    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
+    assert abs(best - float(z["best_score"])) <= LL_TOL
+    assert np.array_equal(smp.best_order, z["best_order"])
+    assert np.array_equal(np.asarray(best_dag), z["best_dag"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    assert np.max(np.abs(smp.parent_weights - z["final_W"])) <= 1e-6
+
+
 def test_trajectory_c2_20():
     z = golden("traj_C2_20.npz")
     m = generator.synthetic_nem(16, 500, 0)

@@ -87,9 +87,9 @@ def test_generator_reproduces_golden_knockdown():
         assert m.A == z["A"] and m.B == z["B"]
 
 
-def _oracle_traj(u, t, order, gamma, swap_prob, n):
+def _oracle_traj(u, t, order, gamma, swap_prob, n, use_nem=False):
     smp = no.OracleSampler(u, t, order)
-    smp.method(swap_prob=swap_prob, gamma=gamma, n_iterations=n)
+    smp.method(swap_prob=swap_prob, gamma=gamma, n_iterations=n, use_nem=use_nem)
     return smp
 
 
@@ -117,4 +117,23 @@ def test_oracle_trajectory_c2_20():
     smp = _oracle_traj(m.U, t, z["order0"], float(z["gamma"]), float(z["swap_prob"]), int(z["n_iter"]))
     assert np.array_equal(np.array(smp.traj["acc"]), z["acc"])
     assert np.array_equal(np.array(smp.all_scores), z["all_scores"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_oracle_trajectory_net2_use_nem_50(net2):
+    """method(use_nem=True) (nem_order_mcmc.py:203-204, 283-284; the closure
+    of utils.py:37-54): the oracle replays the reference's 50-step net2 run."""
+    z = golden("traj_net2_nem_50.npz")
+    tz = golden("net2_tables.npz")
+    assert bool(z["use_nem"])
+    _m, state = net2
+    random.setstate(state)
+    smp = _oracle_traj(tz["U"], tz["T"], z["order0"], float(z["gamma"]), float(z["swap_prob"]),
+                       int(z["n_iter"]), use_nem=True)
+    assert np.array_equal(np.array(smp.traj["acc"]), z["acc"])
+    assert np.array_equal(np.array(smp.traj["perm"]), z["perm"])
+    assert np.array_equal(np.array(smp.all_scores), z["all_scores"])
+    assert smp.best_score == float(z["best_score"])
+    assert np.array_equal(smp.best_order, z["best_order"])
+    assert np.array_equal(smp.w, z["final_W"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
