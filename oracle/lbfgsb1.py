@@ -269,7 +269,7 @@ def minimize_1d(fun, x0, ftol=0.01, gtol=0.01, eps=1e-8, maxls=20, maxiter=15000
                 z = zb
         d = z - x
         # lnsrlb
-        dnorm = math.sqrt(d * d)
+        dnorm = abs(d)  # scipy: dnrm2 (OpenBLAS, extended precision): |d| exactly for n = 1
         stpmx = 1e10
         if cnstnd:
             if nit == 0:

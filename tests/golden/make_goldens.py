@@ -172,12 +172,43 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
             return out
         return orig_loc(self, i, k)
 
+    orig_gow = cls.get_optimal_weights
+    scores = []
+
+    def gow(self, *a, **k):
+        r = orig_gow(self, *a, **k)
+        scores.append(r)
+        return r
+
     cls.get_new_order, cls.accepting, cls.calculate_local_optimum = new_order, accepting, local_opt
+    cls.get_optimal_weights = gow
+    raised = None
     try:
         mc = cls(m, order)
-        best, best_dag = quiet(mc.method, n_iterations=n_iter, gamma=gamma, swap_prob=swap_prob, use_nem=use_nem)
+        try:
+            best, best_dag = quiet(mc.method, n_iterations=n_iter, gamma=gamma, swap_prob=swap_prob,
+                                   use_nem=use_nem)
+        except Exception as exc:  # the reference's own failure (nem_order_mcmc.py:168-169)
+            if not str(exc).startswith("Minimization not successful"):
+                raise
+            raised = str(exc)
     finally:
         cls.get_new_order, cls.accepting, cls.calculate_local_optimum = orig_new, orig_acc, orig_loc
+        cls.get_optimal_weights = orig_gow
+    if raised is not None:
+        # method() raised inside step len(rec["perm"]) (1-based: proposals made);
+        # keep what was decided before it: every proposal, every accept, the
+        # scores of the completed steps (scores[0] is the initial pass, whose
+        # value opt_weights then replaces), the random state at the raise
+        steps = len(rec["acc"])
+        out = dict(order0=np.asarray(order), gamma=gamma, swap_prob=swap_prob, n_iter=n_iter, use_nem=use_nem,
+                   raised=raised, raised_in_step=len(rec["perm"]), steps_completed=steps,
+                   perm=np.array(rec["perm"]), i1=np.array(rec["i1"]), i2=np.array(rec["i2"]),
+                   acc=np.array(rec["acc"]), step_scores=np.array(scores[1:1 + steps]),
+                   W_at_raise=mc.parent_weights, rng_state_at_raise=np.array(random.getstate()[1], dtype=np.int64))
+        np.savez_compressed(os.path.join(HERE, f"traj_{name}.npz"), **out)
+        print(f"traj_{name}: raised in step {len(rec['perm'])} after {steps} completed steps: {raised}")
+        return
     out = dict(order0=np.asarray(order), gamma=gamma, swap_prob=swap_prob, n_iter=n_iter,
                perm=np.array(rec["perm"]), i1=np.array(rec["i1"]), i2=np.array(rec["i2"]),
                acc=np.array(rec["acc"]), all_scores=np.array(mc.all_score_list),

@@ -296,6 +296,61 @@ def test_trajectory_c3(n, max_off):
     assert np.max(np.abs(smp.parent_weights - z["final_W"])) <= 1e-2
 
 
+def _record_sampler(smp):
+    """Per-step proposals, accepts and scores of a mirror sampler, kept even
+    when method() raises (the reference's golden keeps them the same way)."""
+    rec = {"perm": [], "acc": [], "scores": []}
+    new, acc, gow = smp.get_new_order, smp.accepting, smp.get_optimal_weights
+
+    def get_new_order(curr, swap_prob=0.95):
+        r = new(curr, swap_prob=swap_prob)
+        rec["perm"].append(np.array(r[0]))
+        return r
+
+    def accepting(*a):
+        r = acc(*a)
+        rec["acc"].append(bool(r[0]))
+        return r
+
+    def get_optimal_weights(*a, **k):
+        r = gow(*a, **k)
+        rec["scores"].append(r)
+        return r
+
+    smp.get_new_order, smp.accepting, smp.get_optimal_weights = get_new_order, accepting, get_optimal_weights
+    return rec
+
+
+def test_trajectory_c3_until_the_reference_raises():
+    """C3 with the reference's default n_iterations = 500: the reference's own
+    run ends in step 128, when one of that step's local optimisations
+    terminates abnormally and method() raises (nem_order_mcmc.py:168-169;
+    make_goldens.py --only-traj-c3 500).  The mirror makes the same 128
+    proposals and 127 accept decisions, scores every completed step within
+    1e-6 of the reference but at the steps counted below, and raises in the
+    same step."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    z = golden("traj_C3_500.npz")
+    m = generator.synthetic_nem(64, 2000, 0)
+    smp = NEMOrderMCMC(m, z["order0"])
+    rec = _record_sampler(smp)
+    with pytest.raises(Exception, match="Minimization not successful"):
+        smp.method(n_iterations=int(z["n_iter"]), gamma=float(z["gamma"]), swap_prob=float(z["swap_prob"]),
+                   verbose=False)
+    assert len(rec["perm"]) == int(z["raised_in_step"])
+    assert np.array_equal(np.array(rec["perm"]), z["perm"])
+    assert np.array_equal(np.array(rec["acc"]), z["acc"])
+    d = np.abs(np.array(rec["scores"][1:1 + int(z["steps_completed"])]) - z["step_scores"])
+    off = np.where(d > LL_TOL)[0].tolist()
+    print("C3 steps off by more than 1e-6:", off, "max", float(d.max()))
+    assert len(off) <= C3_STEPS_OFF, off
+
+
+# completed C3 steps (of 127) whose score may leave 1e-6 of the reference's
+# (DESIGN.md 3.5): measured on the GPU, asserted exactly
+C3_STEPS_OFF = 1
+
+
 def test_edge_cases():
     # smallest model, E not a multiple of the 64-effect tile, E = 1
     for s, e in ((2, 1), (3, 65), (5, 130)):
