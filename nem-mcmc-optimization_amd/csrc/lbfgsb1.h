@@ -27,6 +27,10 @@
 
 #include <hip/hip_runtime.h>
 
+// the control code is also compiled for the host (tests/host: the exact
+// compact form of lbfgsb_exact.h checked against scipy on the CPU)
+#define NEMO_LB __host__ __device__ __forceinline__
+
 namespace nemo {
 
 struct LbfgsResult {
@@ -41,17 +45,23 @@ constexpr double kSqrtEps = 1.4901161193847656e-08;
 constexpr double kStpMax = 1e10;
 constexpr double kFtolLs = 1e-3, kGtolLs = 0.9, kXtolLs = 0.1;
 
-__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+NEMO_LB double dmax(double a, double b) { return a > b ? a : b; }
 
 // A branch of the optimiser's control flow: its condition is wave-uniform
 // (every lane holds the same f, g and state), so the first lane decides and
 // the compiler emits a scalar branch -- no exec-mask save / restore and no
 // divergent-merge copies of the ~30 state values per branch.
-__device__ __forceinline__ bool uni(bool b) { return __builtin_amdgcn_readfirstlane((int)b) != 0; }
-__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+NEMO_LB bool uni(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane((int)b) != 0;
+#else
+  return b;
+#endif
+}
+NEMO_LB double dmin(double a, double b) { return a < b ? a : b; }
 
 // MINPACK-2 dcstep: safeguarded step and interval update.
-__device__ __forceinline__ void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy,
+NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy,
                               double& dy, double& stp, double fp, double dp, bool& brackt,
                               double stpmin, double stpmax) {
 #pragma clang fp contract(off)
@@ -153,7 +163,7 @@ struct Dcsrch {
   double stpmax = kStpMax;  // lnsrlb's stpmx (1e10 unbounded; from the bounds otherwise)
 
   // returns false on ERROR (initial derivative not negative)
-  __device__ __forceinline__ bool start(double stp, double f, double g) {
+  NEMO_LB bool start(double stp, double f, double g) {
 #pragma clang fp contract(off)
     if (uni(!(g < 0.0))) return false;
     brackt = false;
@@ -172,7 +182,7 @@ struct Dcsrch {
 
   // one dcsrch call with (f, g) at stp; returns 0 = FG (evaluate new stp),
   // 1 = CONV, 2 = WARN
-  __device__ __forceinline__ int step(double& stp, double f, double g) {
+  NEMO_LB int step(double& stp, double f, double g) {
 #pragma clang fp contract(off)
     const double stpmin = 0.0;
     const double ftest = finit + stp * gtest;
