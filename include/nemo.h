@@ -237,7 +237,19 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *   "local_split" 2 = run each local optimum of a fused step on a 4-wave
  *                block (the objective's products split over the waves; same
  *                bits; measured slower for one chain, so 0 = auto never
- *                takes it), 1 = never, 3 = the same on a 2-wave block */
+ *                takes it), 1 = never, 3 = the same on a 2-wave block
+ *   "exact"      1 (default): nemo_optimal_weights, nemo_local_opt and the
+ *                ll-only nemo_score of <= 64 orders compute in the
+ *                reference's own arithmetic -- numpy's SVML log / exp, glibc's
+ *                exp / log1p, numpy's pairwise sum and scipy's compact-form
+ *                L-BFGS-B with OpenBLAS's small kernels, restated bit for bit
+ *                (csrc/refmath.h, csrc/lbfgsb_exact.h, csrc/nemo_exact.hip):
+ *                the same order scores, order weights, local optima and
+ *                weights as nem_order_mcmc.py, to the bit, when "exact_ok";
+ *                0 = the fast kernels (scores within ~1e-9)
+ *   "exact_ok"   (get only) 1 if the staging supports "exact" (factored
+ *                tables, no parent cap, numpy's pairwise sum of E fits the
+ *                wave plan) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 
@@ -256,6 +268,12 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
  *                "i8l_bound", "i8o_bound" (get only): the bound of the log2 /
  *                natural-units kernels for an uncapped call on the staged model */
 int nemo_set_option_f64(nemo_ctx* ctx, const char* name, double value);
+
+/* Test hook: refmath.h's restatements evaluated on the current device, for
+ * the tests that compare them with numpy / scipy bit for bit.  fn: 0 np.log
+ * (SVML), 1 np.exp (SVML), 2 scipy.special.expit, 3 np.logaddexp(x, y),
+ * 4 glibc exp, 5 glibc log1p.  Host arrays of n doubles (y only for fn 3). */
+int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out);
 int nemo_get_option_f64(nemo_ctx* ctx, const char* name, double* value);
 /* which fact_kernel a factored score call with this cap takes (ll_only: no
  * cs / cells / order-weight outputs), with the worst-case |ll error| bound of

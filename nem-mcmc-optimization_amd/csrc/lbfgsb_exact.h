@@ -24,7 +24,7 @@
 // Every product of the 1-D compact form that the library stores (S'Y, S'S,
 // Y'Y, R_z) is one rounded product of two stored scalars, so only the
 // diagonals (s's, s'y), the s / y rings and the factored WN are kept: 540
-// doubles in `mem` (LDS per wave on the device).
+// doubles in `mem` (LDS per wave on the device), with subsm's work vector.
 // Host check: tools/lbfgsb_proto.py found the form (the library's own
 // routines, 2571 / 2571 reference optima bit-equal); tests/test_exact_spec.py
 // runs THIS header on the CPU against the same records.
@@ -42,9 +42,9 @@ using lb::uni;
 constexpr int kM = 10;          // scipy's default memory
 constexpr int kLdN = 2 * kM;    // WN's leading dimension (m2)
 constexpr int kLdT = kM;        // WT's
-constexpr int kMemDoubles = 4 * kM + kLdN * kLdN + kLdT * kLdT;
+constexpr int kMemDoubles = 4 * kM + kLdN * kLdN + kLdT * kLdT + 2 * kM;
 
-// mem layout (doubles): ws[m] wy[m] ssd[m] syd[m] wn[2m x 2m] wt[m x m]
+// mem layout (doubles): ws[m] wy[m] ssd[m] syd[m] wn[2m x 2m] wt[m x m] wv[2m]
 struct Mem {
   double* p;
   NEMO_LB double& ws(int i) { return p[i]; }
@@ -53,6 +53,7 @@ struct Mem {
   NEMO_LB double& syd(int i) { return p[3 * kM + i]; }
   NEMO_LB double* wn() { return p + 4 * kM; }
   NEMO_LB double* wt() { return p + 4 * kM + kLdN * kLdN; }
+  NEMO_LB double* wv() { return p + 4 * kM + kLdN * kLdN + kLdT * kLdT; }
 };
 
 NEMO_LB double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -285,7 +286,7 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta) {
 NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z) {
 #pragma clang fp contract(off)
   const int col = rg.col, c2 = 2 * col;
-  double wv[2 * kM];
+  double* wv = mem.wv();   // (a local array would live in per-lane scratch on the device)
   for (int i = 0; i < col; ++i) {
     wv[i] = sum0(mem.wy(rg.p(i)), r);
     wv[col + i] = theta * sum0(mem.ws(rg.p(i)), r);

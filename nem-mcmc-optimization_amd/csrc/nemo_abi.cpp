@@ -3,6 +3,7 @@
 // No arithmetic of the hot path lives here; it is all in nemo_kernels.hip.
 #include "nemo.h"
 #include "nemo_internal.h"
+#include "refmath.h"
 
 #include <math.h>
 #include <stdarg.h>
@@ -143,7 +144,8 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_wnew, c.d_wdag, c.d_info, c.d_c,    c.d_grows, c.d_gsw,  c.d_gcnt,
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
-                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img};
+                  c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
+                  c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -195,6 +197,8 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_wnew, nc * S * S));
     HIPCHK(dalloc(&c.d_wdag, nc * S * S));
     HIPCHK(dalloc(&c.d_info, nc * S * S));
+    HIPCHK(dalloc(&c.d_xcs, 2 * nc * E));
+    HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
     c.cap_chains = nc;
   }
   return NEMO_OK;
@@ -249,7 +253,8 @@ int alloc_tables(Ctx& c) {
 // the factored form once T's structure is known: every off-diagonal row j is
 // shared by all children and takes lo_j or hi_j (bit d1[j][e] = 1: hi_j)
 int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
-                   const std::vector<double>& elo, const std::vector<double>& ehi) {
+                   const std::vector<double>& elo, const std::vector<double>& ehi,
+                   const std::vector<double>& tlo, const std::vector<double>& thi) {
   Ctx& c = ctx->c;
   const size_t S = c.S, E = c.E;
   const int nwords = (int)((E + 63) / 64);
@@ -304,6 +309,34 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     }
     HIPCHK(nemo::stage_i8o(c, elo, ehi, d1));
     HIPCHK(nemo::stage_window(c, elo, ehi, d1));
+    // the exact path (nemo_exact.hip): numpy's exp of the two values of each
+    // row (the reference's local_vec = np.exp(T[i][k]), restated bit for bit)
+    // and the wave layout of numpy's pairwise sum of E terms
+    c.exact_ok = false;
+    nemo::host::PairwisePlan pl;
+    if (nemo::host::build_pairwise_plan(c.E, pl) && pl.ns <= 4 && pl.nh <= 8) {
+      std::vector<double> xlo(S), xhi(S);
+      for (size_t j = 0; j < S; ++j) {
+        xlo[j] = nemo::refmath::svml_exp(tlo[j]);
+        xhi[j] = nemo::refmath::svml_exp(thi[j]);
+      }
+      std::vector<int32_t> dev;
+      dev.insert(dev.end(), pl.start.begin(), pl.start.end());
+      dev.insert(dev.end(), pl.cnt.begin(), pl.cnt.end());
+      dev.insert(dev.end(), pl.rem.begin(), pl.rem.end());
+      dev.insert(dev.end(), pl.nrem.begin(), pl.nrem.end());
+      dev.insert(dev.end(), pl.partner.begin(), pl.partner.end());
+      HIPCHK(dalloc(&c.d_xlo, S));
+      HIPCHK(dalloc(&c.d_xhi, S));
+      HIPCHK(dalloc(&c.d_pwplan, dev.size()));
+      HIPCHK(hipMemcpy(c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(c.d_pwplan, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+      c.pw_ns = pl.ns;
+      c.pw_nh = pl.nh;
+      c.pw_maxrem = pl.maxrem;
+      c.exact_ok = true;
+    }
   }
   // grow the factored scratch if a batch was reserved before staging
   if (c.cap_batch > 0) {
@@ -365,13 +398,13 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
   // factored form: every off-diagonal row T[.][j] identical for all children
   // and two-valued (nem.py:44-46 builds exactly that); lo_j = its first value
   std::vector<uint64_t> d1;
-  std::vector<double> elo, ehi;
-  bool fact = nemo::host::detect_factored(c.S, c.E, T, d1, elo, ehi);
+  std::vector<double> elo, ehi, tlo, thi;
+  bool fact = nemo::host::detect_factored(c.S, c.E, T, d1, elo, ehi, &tlo, &thi);
   if (!fact) d1.assign((size_t)S * ((E + 63) / 64), 0ull);
   // the factored kernels' exp takes finite arguments: U must be finite too
   for (size_t k = 0; k < (S + 1) * E && fact; ++k)
     if (!isfinite(U[k]) || fabs(U[k]) > 1e9) fact = false;
-  return stage_factored(ctx, fact, d1, elo, ehi);
+  return stage_factored(ctx, fact, d1, elo, ehi, tlo, thi);
 }
 
 int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
@@ -423,9 +456,9 @@ int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
   // factored form straight from D, with nemo_stage_tables' conventions:
   // lo_j = row j's first value, bit = "not lo_j"
   std::vector<uint64_t> d1;
-  std::vector<double> elo, ehi;
-  nemo::host::knockdown_factored(c.S, c.E, D, A, B, d1, elo, ehi);
-  return stage_factored(ctx, ufin, d1, elo, ehi);
+  std::vector<double> elo, ehi, tlo, thi;
+  nemo::host::knockdown_factored(c.S, c.E, D, A, B, d1, elo, ehi, &tlo, &thi);
+  return stage_factored(ctx, ufin, d1, elo, ehi, tlo, thi);
 }
 
 static bool use_factored(const Ctx& c) {
@@ -469,6 +502,26 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
   const size_t S = c.S, E = c.E;
   hipStream_t st = c.stream;
+  if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.exact && cap == 0 && nemo::exact_supported(c) &&
+      batch <= 64) {
+    // ll only for a sampler (calculate_ll / compute_ll of a few orders): the
+    // reference's arithmetic (nemo_exact.hip), pos and W in one copy
+    auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t n = batch, o_w01 = up(n * S * 4), o_ll = o_w01 + up(n * S * S * 8), total = o_ll + up(n * 8);
+    if ((rc = step_stage(c, 0, total))) return rc;
+    char* hs = (char*)c.h_stage[0];
+    char* ds = (char*)c.d_step[0];
+    memcpy(hs, pos, n * S * 4);
+    memcpy(hs + o_w01, w01, n * S * S * 8);
+    HIPCHK(hipMemcpyAsync(ds, hs, o_ll, hipMemcpyHostToDevice, st));
+    HIPCHK(nemo::launch_exact_eval(c, batch, (const int32_t*)ds, (const double*)(ds + o_w01), c.d_ow, c.d_cs,
+                                   (double*)(ds + o_ll), false, st));
+    HIPCHK(hipMemcpyAsync(hs + o_ll, ds + o_ll, n * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(ll_out, hs + o_ll, n * 8);
+    c.ow_chains = 0;  // d_ow no longer holds fused-step order weights
+    return NEMO_OK;
+  }
   if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.step_host_sum && batch <= 64) {
     // ll only (one sampler's calculate_ll): the fused step's transfer pattern --
     // pos and W staged in the pinned slot 0 and sent in ONE copy, the kernel's
@@ -601,7 +654,8 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, 
     cmax = std::max(cmax, cvec[k]);
   }
   const bool prod = c.local_prod && 1.0 + cmin >= 1e-30 && 1.0 + cmax <= 1e30;
-  HIPCHK(nemo::launch_local_opt_generic(c, n, d_c, d_a, d_x, d_o, prod, st));
+  if (c.exact && nemo::exact_supported(c)) HIPCHK(nemo::launch_local_opt_exact_generic(c, n, d_c, d_a, d_x, d_o, st));
+  else HIPCHK(nemo::launch_local_opt_generic(c, n, d_c, d_a, d_x, d_o, prod, st));
   std::vector<double> o((size_t)n * 3);
   HIPCHK(hipMemcpyAsync(o.data(), d_o, n * 3 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipFreeAsync(d_c, st));
@@ -649,6 +703,20 @@ int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, co
     return fail(NEMO_ERR_ARG, "null device pointer");
   hipStream_t st = pick(ctx, stream);
   const int npairs = nemo::pairs_per_chain(c.S, cap);
+  if (use_factored(c) && c.exact && cap == 0 && nemo::exact_supported(c)) {
+    // the reference's own arithmetic (nemo_exact.hip): eval #1's cells and
+    // order weights in d_ow, the local optima (eval #1's ll summed by the
+    // launch's appended blocks), eval #2 summed on the device
+    double* cs1 = c.d_xcs;
+    double* cs2 = c.d_xcs + (size_t)nchains * c.E;
+    HIPCHK(nemo::launch_step_prep(c, nchains, cap, d_pos, d_w01, d_info, st));
+    HIPCHK(nemo::launch_exact_eval(c, nchains, d_pos, d_w01, c.d_ow, cs1, nullptr, true, st));
+    HIPCHK(nemo::launch_local_opt_exact(c, nchains, npairs, c.d_pairs, d_w01, d_anc, c.d_ow, sig0, sig1, d_w_new,
+                                        c.d_wdag, d_info, cs1, d_ll1, st));
+    HIPCHK(nemo::launch_exact_eval(c, nchains, d_pos, c.d_wdag, c.d_xcells2, cs2, d_ll_dag, false, st));
+    c.ow_chains = nchains;
+    return NEMO_OK;
+  }
   // eval #1 with order weights (nem_order_mcmc.py:181-182).  Factored: one
   // prep launch for the pair lists (info rows preset to -1) and eval #1's
   // Delta, and eval #1's partial sums ride in the local-optimum launch -- two
@@ -1081,6 +1149,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
   if (rc) return rc;
   if (!name) return fail(NEMO_ERR_ARG, "null option name");
   ++ctx->c.graph_epoch;  // any option may change what a captured step launches
+  if (strcmp(name, "exact") == 0) {
+    ctx->c.exact = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "graphs") == 0) {
     ctx->c.graphs = value ? 1 : 0;
     return NEMO_OK;
@@ -1136,10 +1208,32 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "i8w") == 0) *value = c.i8w_ok ? 1 : 0;
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "graphs") == 0) *value = c.graphs;
+  else if (strcmp(name, "exact") == 0) *value = c.exact;
+  else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;
   else if (strcmp(name, "step_host_sum") == 0) *value = c.step_host_sum;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;
   else if (strcmp(name, "local_prod") == 0) *value = c.local_prod && c.table_absmax <= 40.0 ? 1 : 0;
   else return fail(NEMO_ERR_ARG, "unknown option '%s'", name);
+  return NEMO_OK;
+}
+
+int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out) {
+  if (n < 0 || fn < 0 || fn > 5 || (n > 0 && (!x || !out || (fn == 3 && !y))))
+    return fail(NEMO_ERR_ARG, "fn=%d n=%d / null pointer", fn, n);
+  if (n == 0) return NEMO_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(NEMO_ERR_HIP, "no HIP device visible");
+  double *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc((void**)&dx, (size_t)n * 8));
+  HIPCHK(hipMalloc((void**)&dout, (size_t)n * 8));
+  if (fn == 3) HIPCHK(hipMalloc((void**)&dy, (size_t)n * 8));
+  HIPCHK(hipMemcpy(dx, x, (size_t)n * 8, hipMemcpyHostToDevice));
+  if (dy) HIPCHK(hipMemcpy(dy, y, (size_t)n * 8, hipMemcpyHostToDevice));
+  HIPCHK(nemo::launch_refmath_probe(fn, n, dx, dy, dout, nullptr));
+  HIPCHK(hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipFree(dx));
+  HIPCHK(hipFree(dout));
+  if (dy) HIPCHK(hipFree(dy));
   return NEMO_OK;
 }
 

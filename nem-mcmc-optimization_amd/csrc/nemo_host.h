@@ -51,11 +51,14 @@ inline int first_bad_pos_row(const int32_t* pos, int batch, int S) {
 // d1 [S][nwords] (nwords = ceil(E / 64)), elo / ehi [S] = exp(lo_j), exp(hi_j).
 // Returns false (outputs unspecified) when T lacks that structure.
 inline bool detect_factored(int S, int E, const double* T, std::vector<uint64_t>& d1, std::vector<double>& elo,
-                            std::vector<double>& ehi) {
+                            std::vector<double>& ehi, std::vector<double>* tlo = nullptr,
+                            std::vector<double>* thi = nullptr) {
   const int nwords = (E + 63) / 64;
   d1.assign((size_t)S * nwords, 0ull);
   elo.assign(S, 0.0);
   ehi.assign(S, 0.0);
+  if (tlo) tlo->assign(S, 0.0);
+  if (thi) thi->assign(S, 0.0);
   for (int j = 0; j < S; ++j) {
     const int i0 = (j == 0) ? 1 : 0;
     const double* L = T + ((size_t)i0 * S + j) * E;
@@ -76,6 +79,8 @@ inline bool detect_factored(int S, int E, const double* T, std::vector<uint64_t>
     }
     elo[j] = std::exp(lo);
     ehi[j] = std::exp(hi);
+    if (tlo) (*tlo)[j] = lo;
+    if (thi) (*thi)[j] = hi;
   }
   return true;
 }
@@ -83,11 +88,14 @@ inline bool detect_factored(int S, int E, const double* T, std::vector<uint64_t>
 // the same from the knockdown matrix D [S][E] in {0,1} (nem.py:25-64): row j
 // of T is where(D[j] == 0, B, -A), so lo_j = (D[j][0] ? -A : B)
 inline void knockdown_factored(int S, int E, const uint8_t* D, double A, double B, std::vector<uint64_t>& d1,
-                               std::vector<double>& elo, std::vector<double>& ehi) {
+                               std::vector<double>& elo, std::vector<double>& ehi,
+                               std::vector<double>* tlo = nullptr, std::vector<double>* thi = nullptr) {
   const int nwords = (E + 63) / 64;
   d1.assign((size_t)S * nwords, 0ull);
   elo.assign(S, 0.0);
   ehi.assign(S, 0.0);
+  if (tlo) tlo->assign(S, 0.0);
+  if (thi) thi->assign(S, 0.0);
   const double negA = -A;
   for (int j = 0; j < S; ++j) {
     const uint8_t* r = D + (size_t)j * E;
@@ -101,7 +109,79 @@ inline void knockdown_factored(int S, int E, const uint8_t* D, double A, double 
     }
     elo[j] = std::exp(lo);
     ehi[j] = std::exp(hi);
+    if (tlo) (*tlo)[j] = lo;
+    if (thi) (*thi)[j] = hi;
   }
+}
+
+// ---------------------------------------------------------------------------
+// numpy's pairwise summation of an E-vector (DOUBLE_pairwise_sum, blocks of
+// <= 128 with 8 accumulators, halving at multiples of 8) laid out over one
+// wave for the exact local optimum (nemo_exact.hip): leaf block L (in order)
+// owns 8 accumulator chains -- lanes 8 (L % 8) .. + 7 of register slot L / 8
+// -- each chain its elements start + k + 8 m, its block's n % 8 trailing
+// elements one per lane of the same group, and the recursion's additions run
+// as one level per height, the node's value at its first leaf's lane.
+// ---------------------------------------------------------------------------
+struct PairwisePlan {
+  int E = 0, nleaf = 0, ns = 0, nh = 0, maxrem = 0;
+  // [ns][64] per (slot, lane): chain start element (-1: none), its element
+  // count, the group's trailing element of this lane (-1: none), the group's
+  // trailing count; [nh][64]: the lane whose value to add at that height (-1)
+  std::vector<int32_t> start, cnt, rem, nrem, partner;
+};
+
+inline bool build_pairwise_plan(int E, PairwisePlan& pl) {
+  struct Leaf { long s, n; };
+  std::vector<Leaf> leaves;
+  struct Op { int h, lane, partner; };
+  std::vector<Op> ops;
+  // returns (first leaf, height)
+  std::function<std::pair<int, int>(long, long)> rec = [&](long s, long n) -> std::pair<int, int> {
+    if (n <= 128) {
+      leaves.push_back({s, n});
+      return {(int)leaves.size() - 1, 0};
+    }
+    long n2 = n / 2;
+    n2 -= n2 % 8;
+    const auto l = rec(s, n2);
+    const auto r = rec(s + n2, n - n2);
+    const int h = 1 + std::max(l.second, r.second);
+    ops.push_back({h, l.first, r.first});
+    return {l.first, h};
+  };
+  if (E < 1) return false;
+  const int root_h = rec(0, E).second;
+  pl = PairwisePlan{};
+  pl.E = E;
+  pl.nleaf = (int)leaves.size();
+  if (pl.nleaf > 64) return false;  // one leaf result per lane for the tree
+  pl.ns = (8 * pl.nleaf + 63) / 64;
+  pl.nh = root_h;
+  pl.start.assign((size_t)pl.ns * 64, -1);
+  pl.cnt.assign((size_t)pl.ns * 64, 0);
+  pl.rem.assign((size_t)pl.ns * 64, -1);
+  pl.nrem.assign((size_t)pl.ns * 64, 0);
+  pl.partner.assign((size_t)std::max(pl.nh, 1) * 64, -1);
+  for (int L = 0; L < pl.nleaf; ++L) {
+    const long s = leaves[L].s, n = leaves[L].n;
+    const int u = L / 8, base = 8 * (L % 8);
+    const long full = n >= 8 ? n - n % 8 : 0;   // n < 8 (E < 8): no chains, sum from 0.0
+    const int nr = (int)(n - full);
+    if (nr > 7) return false;
+    pl.maxrem = std::max(pl.maxrem, nr);
+    for (int k = 0; k < 8; ++k) {
+      const size_t q = (size_t)u * 64 + base + k;
+      if (full) {
+        pl.start[q] = (int32_t)(s + k);
+        pl.cnt[q] = (int32_t)(full / 8);
+      }
+      pl.rem[q] = k < nr ? (int32_t)(s + full + k) : -1;
+      pl.nrem[q] = nr;
+    }
+  }
+  for (const Op& o : ops) pl.partner[(size_t)(o.h - 1) * 64 + o.lane] = o.partner;
+  return true;
 }
 
 // the two addition chains of compute_scores (nem.py:25-34), in its order:

@@ -110,6 +110,18 @@ struct Ctx {
   double* d_wuw = nullptr;         // [S][2] U - U[S] of row i at D1 bit 0 / 1
   double* d_wnull = nullptr;       // [nwords] sum of U[S][e] over each 64-effect word
 
+  // the reference's own arithmetic in the fused step and the sampler's ll-only
+  // calls (nemo_exact.hip): option "exact" (1 default), available when the
+  // staged model is factored and numpy's pairwise sum of E fits the wave plan
+  int exact = 1;
+  bool exact_ok = false;
+  double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
+  double* d_xhi = nullptr;         // [S] numpy's exp(hi_j)
+  int32_t* d_pwplan = nullptr;     // host::PairwisePlan of E, device layout
+  int pw_ns = 0, pw_nh = 0, pw_maxrem = 0;
+  double* d_xcs = nullptr;         // [2][chains][E] cs of the step's two evaluations
+  double* d_xcells2 = nullptr;     // [chains][S+1][E] eval #2's cells
+
   // worst-case |ll error| of the fixed-point kernels (nemo_host.h):
   // fx_colsum[k] = sum_e min(colbits_e, k) over the staged D1 bits; auto takes
   // a fixed-point kernel only while its bound stays within err_budget
@@ -214,6 +226,26 @@ hipError_t launch_local_opt_pairs(Ctx& c, int nchains, int npairs, const int32_t
 // e in (0, 1), within [1e-30, 1e30]; the caller checks)
 hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const double* d_anc,
                                     const double* d_x0, double* d_out, bool prod, hipStream_t st);
+
+// the reference's arithmetic (nemo_exact.hip): supported for this staging?
+bool exact_supported(const Ctx& c);
+// eval in the reference's order: cells into d_cells [batch][S+1][E] (with
+// want_ow: replaced by the order weights), cs into d_cs [batch][E], ll into
+// d_ll (nullable: left to the caller)
+hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
+                             double* d_cs, double* d_ll, bool want_ow, hipStream_t st);
+// every permissible pair's exact local optimum; the appended blocks sum d_cs1
+// into d_ll1 (eval #1's ll) when d_ll1 is set
+hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t* d_pairs, const double* d_w01,
+                                  const double* d_anc, const double* d_ow, double sig0, double sig1, double* d_wnew,
+                                  double* d_wdag, int32_t* d_info, const double* d_cs1, double* d_ll1,
+                                  hipStream_t st);
+
+// nemo_local_opt in the reference's arithmetic (out [n][3] as local_opt_generic)
+hipError_t launch_local_opt_exact_generic(Ctx& c, int n, const double* d_c, const double* d_anc, const double* d_x0,
+                                          double* d_out, hipStream_t st);
+// refmath.h on the device, for the tests (nemo_refmath_probe)
+hipError_t launch_refmath_probe(int fn, int n, const double* d_x, const double* d_y, double* d_out, hipStream_t st);
 
 // number of (child, parent) pairs per chain for a given cap
 int pairs_per_chain(int S, int cap);

@@ -29,8 +29,10 @@
 
 #if defined(__HIPCC__)
 #define NEMO_RM __host__ __device__ __forceinline__
+#define NEMO_RMM __host__ __device__ __forceinline__
 #else
 #define NEMO_RM static inline
+#define NEMO_RMM inline
 #endif
 
 #if defined(__clang__)
@@ -43,8 +45,35 @@ namespace nemo {
 namespace refmath {
 
 NEMO_RM double as_double(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+// Where the functions read their tables: by default the constant arrays of
+// refmath_tables.h; a device kernel passes copies in LDS (per-lane indices)
+struct ConstTabs {
+  NEMO_RMM double log_hi(int j) const;
+  NEMO_RMM double log_lo(int j) const;
+  NEMO_RMM double exp_hi(int j) const;
+  NEMO_RMM double exp_lo(int j) const;
+  NEMO_RMM uint64_t gexp(int i) const;
+};
+struct LdsTabs {
+  const double* log_hi_p;   // [16]
+  const double* log_lo_p;   // [16]
+  const double* exp_hi_p;   // [16]
+  const double* exp_lo_p;   // [16]
+  const uint64_t* gexp_p;   // [256]
+  NEMO_RMM double log_hi(int j) const { return log_hi_p[j]; }
+  NEMO_RMM double log_lo(int j) const { return log_lo_p[j]; }
+  NEMO_RMM double exp_hi(int j) const { return exp_hi_p[j]; }
+  NEMO_RMM double exp_lo(int j) const { return exp_lo_p[j]; }
+  NEMO_RMM uint64_t gexp(int i) const { return gexp_p[i]; }
+};
 NEMO_RM uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
 NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+NEMO_RMM double ConstTabs::log_hi(int j) const { return as_double(kSvmlLogHi[j]); }
+NEMO_RMM double ConstTabs::log_lo(int j) const { return as_double(kSvmlLogLo[j]); }
+NEMO_RMM double ConstTabs::exp_hi(int j) const { return as_double(kSvmlExpHi[j]); }
+NEMO_RMM double ConstTabs::exp_lo(int j) const { return as_double(kSvmlExpLo[j]); }
+NEMO_RMM uint64_t ConstTabs::gexp(int i) const { return kGlibcExpTab[i]; }
 
 // ---------------------------------------------------------------------------
 // glibc 2.35 exp (sysdeps/ieee754/dbl-64/e_exp.c, Szabolcs Nagy's table
@@ -65,9 +94,9 @@ NEMO_RM double glibc_exp_special(double tmp, uint64_t sbits, uint64_t ki) {
   // k < 0: the subnormal range, rounded once
   sbits += 1022ull << 52;
   const double scale = as_double(sbits);
-  double y = scale + scale * tmp;  // not fused in __exp_fma's specialcase (measured)
+  double y = scale + scale * tmp;  // __exp_fma's specialcase is not fused (measured)
   if (y < 1.0) {
-    double lo = fma_(scale, tmp, scale - y);
+    double lo = (scale - y) + scale * tmp;
     const double hi = 1.0 + y;
     lo = ((1.0 - hi) + y) + lo;
     y = (hi + lo) - 1.0;
@@ -76,7 +105,8 @@ NEMO_RM double glibc_exp_special(double tmp, uint64_t sbits, uint64_t ki) {
   return 0x1p-1022 * y;
 }
 
-NEMO_RM double glibc_exp(double x) {
+template <class TB = ConstTabs>
+NEMO_RM double glibc_exp(double x, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
   constexpr double kInvLn2N = 0x1.71547652b82fep0 * 128;
   constexpr double kShift = 0x1.8p52;
@@ -101,8 +131,8 @@ NEMO_RM double glibc_exp(double x) {
   const double r = fma_(kd, kNegLn2loN, fma_(kd, kNegLn2hiN, x));
   const uint64_t idx = 2 * (ki % 128);
   const uint64_t top = ki << 45;
-  const double tail = as_double(kGlibcExpTab[idx]);
-  const uint64_t sbits = kGlibcExpTab[idx + 1] + top;
+  const double tail = as_double(tb.gexp((int)idx));
+  const uint64_t sbits = tb.gexp((int)idx + 1) + top;
   const double r2 = r * r;
   const double tmp = fma_(r2 * r2, fma_(r, C5, C4), fma_(r2, fma_(r, C3, C2), tail + r));
   if (abstop == 0) return glibc_exp_special(tmp, sbits, ki);
@@ -112,9 +142,10 @@ NEMO_RM double glibc_exp(double x) {
 
 // scipy.special.expit for float64: 1 / (1 + exp(-x)) (scipy 1.15 special,
 // std::exp = glibc exp)
-NEMO_RM double expit(double x) {
+template <class TB = ConstTabs>
+NEMO_RM double expit(double x, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
-  return 1.0 / (1.0 + glibc_exp(-x));
+  return 1.0 / (1.0 + glibc_exp(-x, tb));
 }
 
 // ---------------------------------------------------------------------------
@@ -194,13 +225,14 @@ NEMO_RM double glibc_log1p(double x) {
 }
 
 // numpy's npy_logaddexp (npymath, float64): glibc exp and log1p
-NEMO_RM double logaddexp(double x, double y) {
+template <class TB = ConstTabs>
+NEMO_RM double logaddexp(double x, double y, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
   constexpr double kLogE2 = 0.693147180559945309417232121458176568;
   if (x == y) return x + kLogE2;
   const double tmp = x - y;
-  if (tmp > 0) return x + glibc_log1p(glibc_exp(-tmp));
-  if (tmp <= 0) return y + glibc_log1p(glibc_exp(tmp));
+  if (tmp > 0) return x + glibc_log1p(glibc_exp(-tmp, tb));
+  if (tmp <= 0) return y + glibc_log1p(glibc_exp(tmp, tb));
   return tmp;
 }
 
@@ -211,7 +243,8 @@ NEMO_RM double logaddexp(double x, double y) {
 // r < 0.75, evaluated as below.  For positive normal x (the path's logs:
 // arguments 1 + c e and 1 - w + w e^T).
 // ---------------------------------------------------------------------------
-NEMO_RM double svml_log(double x) {
+template <class TB = ConstTabs>
+NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
   constexpr double C180 = 0x1.c81cd309d7c70p-4, C1c0 = -0x1.007357e93af62p-3;
   constexpr double C200 = 0x1.249229cee81efp-3, C240 = -0x1.55553fb28db06p-3;
@@ -237,13 +270,13 @@ NEMO_RM double svml_log(double x) {
   p1 = fma_(R2, p1, p7);
   const double R4 = R2 * R2;
   p9 = fma_(R2, p9, p8);
-  const double H = fma_(k, kLn2Hi, as_double(kSvmlLogHi[j]));
+  const double H = fma_(k, kLn2Hi, tb.log_hi(j));
   const double P = fma_(R4, p1, p9);
   const double S = H + R;
   const double D = S - H;
   const double E = R - D;
   const double Q = fma_(R2, P, E);
-  const double L = fma_(kLn2Lo, k, as_double(kSvmlLogLo[j]));
+  const double L = fma_(kLn2Lo, k, tb.log_lo(j));
   return S + (Q + L);
 }
 
@@ -258,7 +291,8 @@ NEMO_RM double svml_log(double x) {
 // order weights exp(cell - cs) of negligible rows, whose c = a / b then
 // enters log(c e + 1) as 1 + tiny = 1 either way).
 // ---------------------------------------------------------------------------
-NEMO_RM double svml_exp(double x) {
+template <class TB = ConstTabs>
+NEMO_RM double svml_exp(double x, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
   constexpr double kLog2e = 0x1.71547652b82fep+0;
   constexpr double kS = 0x1.8000000003ff0p+48;
@@ -288,8 +322,8 @@ NEMO_RM double svml_exp(double x) {
   const double p11 = fma_(r, C340, C380);
   p12 = fma_(r2, p12, p9);
   p12 = fma_(r2, p12, p11);
-  const double thi = as_double(kSvmlExpHi[j]);
-  const double q = fma_(p12, r, as_double(kSvmlExpLo[j]));
+  const double thi = tb.exp_hi(j);
+  const double q = fma_(p12, r, tb.exp_lo(j));
   const double y = fma_(thi, q, thi);
   const double kfl = __builtin_floor(kf);
   return __builtin_ldexp(y, (int)kfl);

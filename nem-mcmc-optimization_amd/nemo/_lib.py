@@ -66,6 +66,7 @@ SIGNATURES = [
     ("nemo_score_kernel", C.c_int, [_vp, C.c_int, C.c_int, _i32p, _f64p]),
     ("nemo_timing_enable", C.c_int, [_vp, C.c_int]),
     ("nemo_timing_read", C.c_int, [_vp, _f64p, _i32p]),
+    ("nemo_refmath_probe", C.c_int, [C.c_int, C.c_int, _f64p, _f64p, _f64p]),
 ]
 
 
@@ -138,3 +139,17 @@ def device_count() -> int:
     n = C.c_int32(0)
     check(load().nemo_device_count(C.byref(n)))
     return n.value
+
+
+REFMATH_FNS = {"log": 0, "exp": 1, "expit": 2, "logaddexp": 3, "glibc_exp": 4, "glibc_log1p": 5}
+
+
+def refmath_probe(fn: str, x, y=None) -> np.ndarray:
+    """csrc/refmath.h's restatement ``fn`` evaluated on the device (test hook:
+    numpy's np.log / np.exp, scipy's expit, np.logaddexp, glibc's exp and
+    log1p, bit for bit)."""
+    x = f64(x).ravel()
+    y = None if y is None else f64(y).ravel()
+    out = np.empty_like(x)
+    check(load().nemo_refmath_probe(REFMATH_FNS[fn], x.size, ptr(x), ptr(y), ptr(out)))
+    return out

@@ -95,3 +95,98 @@ void spec_logaddexp(long n, const double* x, const double* y, double* z) {
 double spec_pairwise_sum(long n, const double* a) { return pairwise_sum(a, n); }
 
 }  // extern "C"
+
+extern "C" {
+
+// compute_cell_ratios + calculate_ll (nem_order_mcmc.py:79-93) as numpy runs
+// them, for one order: cells (S+1) x E, cs = logaddexp.reduce over the rows,
+// ow = exp(cell - cs), ll = sum(cs) (Python's left fold); T is S x S x E,
+// perm the order, w_raw S x S (expit applied here, as the reference does)
+double spec_eval(int S, int E, const double* U, const double* T, const int32_t* perm, const double* w_raw,
+                 double* cells, double* cs, double* ow) {
+#pragma clang fp contract(off)
+  int* pos = new int[S];
+  for (int q = 0; q < S; ++q) pos[perm[q]] = q;
+  for (long k = 0; k < (long)(S + 1) * E; ++k) cells[k] = U[k];
+  for (int i = 0; i < S; ++i)
+    for (int q = 0; q < pos[i]; ++q) {
+      const int j = perm[q];
+      const double s = refmath::expit(w_raw[(long)i * S + j]);
+      const double oms = 1.0 - s;
+      const double* t = T + ((long)i * S + j) * E;
+      double* c = cells + (long)i * E;
+      for (int e = 0; e < E; ++e) c[e] += refmath::svml_log(oms + s * refmath::svml_exp(t[e]));
+    }
+  double ll = 0.0;
+  for (int e = 0; e < E; ++e) {
+    double acc = cells[e];
+    for (int r = 1; r <= S; ++r) acc = refmath::logaddexp(acc, cells[(long)r * E + e]);
+    cs[e] = acc;
+    ll = ll + acc;
+  }
+  for (int r = 0; r <= S; ++r)
+    for (int e = 0; e < E; ++e) ow[(long)r * E + e] = refmath::svml_exp(cells[(long)r * E + e] - cs[e]);
+  delete[] pos;
+  return ll;
+}
+
+}  // extern "C"
+
+#include "nemo_host.h"
+
+extern "C" {
+
+// host::build_pairwise_plan run as the device runs it (nemo_exact.hip's
+// ExactObjective::sum_logs, lanes as arrays): numpy's pairwise sum of a[E]?
+// Returns the sum, or NaN when the plan does not fit.
+double spec_plan_sum(int E, const double* a) {
+#pragma clang fp contract(off)
+  nemo::host::PairwisePlan pl;
+  if (!nemo::host::build_pairwise_plan(E, pl)) return __builtin_nan("");
+  const int NS = pl.ns;
+  std::vector<double> res((size_t)NS * 64);
+  for (int u = 0; u < NS; ++u) {
+    double acc[64], tr[64];
+    for (int l = 0; l < 64; ++l) {
+      const size_t q = (size_t)u * 64 + l;
+      const int st = pl.start[q], ct = pl.cnt[q];
+      double v = ct > 0 ? a[st] : 0.0;
+      for (int m = 1; m < ct; ++m) v = v + a[st + 8 * m];
+      acc[l] = v;
+      tr[l] = pl.rem[q] >= 0 ? a[pl.rem[q]] : 0.0;
+    }
+    for (int d : {1, 2, 4}) {
+      double nx[64];
+      for (int l = 0; l < 64; ++l) nx[l] = acc[l] + acc[l ^ d];
+      for (int l = 0; l < 64; ++l) acc[l] = nx[l];
+    }
+    for (int l = 0; l < 64; ++l) {
+      const int nr = pl.nrem[(size_t)u * 64 + l];
+      for (int r = 0; r < nr; ++r) acc[l] = acc[l] + tr[(l & ~7) + r];
+      res[(size_t)u * 64 + l] = acc[l];
+    }
+  }
+  double v[64];
+  for (int l = 0; l < 64; ++l) v[l] = (l >> 3) < NS ? res[(size_t)(l >> 3) * 64 + 8 * (l & 7)] : 0.0;
+  for (int h = 0; h < pl.nh; ++h) {
+    double nx[64];
+    for (int l = 0; l < 64; ++l) {
+      const int p = pl.partner[(size_t)h * 64 + l];
+      nx[l] = p >= 0 ? v[l] + v[p] : v[l];
+    }
+    for (int l = 0; l < 64; ++l) v[l] = nx[l];
+  }
+  return v[0];
+}
+
+int spec_plan_shape(int E, int32_t* out4) {
+  nemo::host::PairwisePlan pl;
+  if (!nemo::host::build_pairwise_plan(E, pl)) return -1;
+  out4[0] = pl.nleaf;
+  out4[1] = pl.ns;
+  out4[2] = pl.nh;
+  out4[3] = pl.maxrem;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+"""GPU: the fused step in the reference's own arithmetic (option "exact",
+the default; csrc/refmath.h, csrc/lbfgsb_exact.h, csrc/nemo_exact.hip),
+checked bit for bit -- no tolerance -- against numpy / scipy and against the
+reference's own recorded outputs."""
+import math
+import random
+
+import numpy as np
+import pytest
+from conftest import golden
+from scipy.special import expit
+
+import nemo_oracle as no
+from nemo import _lib, generator
+from nemo.engine import Engine
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_equal(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def test_refmath_on_the_device_equals_numpy_scipy_glibc():
+    """np.log / np.exp (SVML), scipy's expit, np.logaddexp and glibc's exp /
+    log1p: the device restatements give the libraries' bits."""
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    x = np.exp(rng.uniform(np.log(1e-3), np.log(1e6), n))
+    assert _bits_equal(_lib.refmath_probe("log", x), np.log(x))
+    x = 1.0 + np.exp(rng.uniform(np.log(1e-12), np.log(1e-2), n))
+    assert _bits_equal(_lib.refmath_probe("log", x), np.log(x))
+    x = rng.uniform(-707, 707, n)
+    assert _bits_equal(_lib.refmath_probe("exp", x), np.exp(x))
+    x = rng.uniform(-50, 0, n)
+    assert _bits_equal(_lib.refmath_probe("exp", x), np.exp(x))
+    x = rng.normal(0, 6, n)
+    assert _bits_equal(_lib.refmath_probe("expit", x), expit(x))
+    a, b = rng.normal(-60, 25, n), rng.normal(-60, 25, n)
+    b[::7] = a[::7]
+    assert _bits_equal(_lib.refmath_probe("logaddexp", a, b), np.logaddexp(a, b))
+    x = rng.uniform(-745, 709, 1 << 16)
+    assert _bits_equal(_lib.refmath_probe("glibc_exp", x), [math.exp(v) for v in x])
+    x = np.exp(rng.uniform(np.log(1e-300), 0, 1 << 16))
+    assert _bits_equal(_lib.refmath_probe("glibc_log1p", x), [math.log1p(v) for v in x])
+
+
+@pytest.mark.parametrize("name", ["net2_200", "C2_20"])
+def test_exact_local_optima_equal_scipy_records(name):
+    """Every recorded reference optimisation (c, anc, x0 -> scipy's x*, f*,
+    nit, nfev): the same bits."""
+    z = golden(f"localopt_{name}.npz")
+    e = z["c"].shape[1]
+    eng = Engine(np.zeros((3, e)), np.zeros((2, 2, e)))
+    assert eng.get_option("exact") == 1 and eng.get_option("exact_ok") == 1
+    xs, fs, nit, nfev, st = eng.local_opt(z["c"], z["anc"], z["x0"])
+    assert np.array_equal(nit, z["nit"]) and np.array_equal(nfev, z["nfev"])
+    assert _bits_equal(xs, z["xstar"]), int((xs != z["xstar"]).sum())
+    assert _bits_equal(fs, z["fun"])
+    eng.close()
+
+
+@pytest.mark.parametrize("name,s,e", [("C2", 16, 500), ("C3", 64, 2000)])
+def test_exact_scores_equal_reference_goldens(name, s, e):
+    """calculate_ll of the golden orders and weights (<= 64 orders: a
+    sampler's ll-only call): the reference's ll to the bit."""
+    z = golden(f"eval_{name}.npz")
+    m = generator.synthetic_nem(s, e, 0)
+    eng = Engine.for_nem(m)
+    pos = np.array([np.argsort(p) for p in z["perm"]], dtype=np.int32)
+    ll = eng.score(pos, expit(z["W"]))
+    assert _bits_equal(ll, z["ll"])
+    eng.close()
+
+
+def test_exact_fused_step_equals_oracle_c3():
+    """One get_optimal_weights at 64 x 2000 (2016 local optima) against the
+    oracle, i.e. numpy and scipy: every weight, ll and dag_ll to the bit."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    t = m.get_score_tensor()
+    rng = np.random.default_rng(12)
+    perm = rng.permutation(m.num_s)
+    smp = NEMOrderMCMC(m, perm, engine=eng)
+    w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
+    smp.parent_weights = w_raw.copy()
+    ora = no.OracleSampler(m.U, t, perm)
+    ora.w = w_raw.copy()
+    ref_dag = ora.optimal_weights()
+    got_dag = smp.get_optimal_weights(init=True)
+    assert smp.ll == ora.ll1
+    assert _bits_equal(smp.parent_weights, ora.w)
+    assert got_dag == ref_dag
+    eng.close()
+
+
+def test_exact_chain_batch_equals_single_chains():
+    """Batched chains (one fused call per step for all) give every chain the
+    bits of its own single-chain run, in the exact arithmetic too."""
+    from nemo.chains import ChainBatch
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(16, 500, 0)
+    eng = Engine.for_nem(m)
+    order = np.arange(16)
+    cb = ChainBatch(m, [order] * 5, seeds=list(range(5)), engine=eng, on_fail="continue")
+    best, _ = cb.run(6)
+    for c in (0, 3):
+        smp = NEMOrderMCMC(m, order, engine=eng)
+        smp.rng = random.Random(c)
+        b1, _ = smp.method(n_iterations=6, gamma=2.0 * 16 / 500, swap_prob=0.95, verbose=False)
+        assert b1 == best[c]
+        assert _bits_equal(smp.parent_weights, cb.chains[c].parent_weights)
+    eng.close()
