@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round pass: smoke, GPU tests, parity statistics, bench (with C4), then the
+# Final pass: tools/gpu_round.sh (smoke, GPU tests, the traced bench, PMC), then the
 # rocprofv3 kernel traces and PMC passes whose records bench.py attaches
 # (C3 with stall counters, W128, C5, and the streaming kernel at B = 128).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 P=${PROF_DIR:-gpurun_out/final}
-PROF_DIR=$P bash tools/gpu_r3.sh || exit 1
+PROF_DIR=$P PMC=1 bash tools/gpu_round.sh || exit 1
 PROF_DIR=$P/c3 STALLS=1 bash tools/gpu_prof.sh || exit 1
 PROF_DIR=$P/w128 CONFIG=W128 bash tools/gpu_prof.sh || exit 1
 PROF_DIR=$P/c5 CONFIG=C5 bash tools/gpu_prof.sh || exit 1
