@@ -598,15 +598,31 @@ def main():
         pos_h = pos[:nch]
         w_h = rng.uniform(-3, 3, (nch, S, S))
         anc = np.clip(rng.random((nch, S, S)) - 0.5, 0, 1)
-        eng.optimal_weights(pos_h, expit(w_h), anc, w_h, SIG0, SIG1, cap=cap, raise_on_fail=False)
-        ts = []
-        for _ in range(5):
-            t0 = time.perf_counter()
-            eng.optimal_weights(pos_h, expit(w_h), anc, w_h, SIG0, SIG1, cap=cap, raise_on_fail=False)
-            ts.append(time.perf_counter() - t0)
-        fs = float(np.median(ts))
+        def fused_ms(nc, reps):
+            eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
+                                raise_on_fail=False)
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
+                                    raise_on_fail=False)
+                ts.append(time.perf_counter() - t0)
+            return float(np.median(ts))
+
+        # the default step computes in the reference's own arithmetic ("exact":
+        # the same bits as numpy / scipy); the fast kernels
+        # beside it (scores within ~1e-9, a few optima per C3 step on another
+        # line-search path)
+        exact_on = bool(eng.get_option("exact")) and bool(eng.get_option("exact_ok"))
+        fs = fused_ms(nch, 5)
+        eng.set_option("exact", 0)
+        fs_fast = fused_ms(nch, 5)
+        fs1_fast = fused_ms(1, 20)
+        eng.set_option("exact", 1)
         extras["mcmc_fused_step"] = {
             "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
+            "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
+            "fast_kernels_ms_per_step": 1e3 * fs_fast,
             "includes": "H2D of pos/W/anc, eval#1 with order weights, 2016 L-BFGS-B local optima "
                         "per chain, eval#2 on binarised weights, D2H"}
         # BASELINE C3 names ONE chain: what one chain sees per call -- a
@@ -626,6 +642,7 @@ def main():
         extras["single_chain"] = {
             "score_call_us": 1e6 * float(np.median(lat)), "evals_per_s_sequential": 1.0 / float(np.median(lat)),
             "fused_step_ms": 1e3 * float(np.median(ts1)), "chain_steps_per_s": 1.0 / float(np.median(ts1)),
+            "fused_step_ms_fast_kernels": 1e3 * fs1_fast,
             "reference_cpu_s_per_chain_step": 1.2,
             "includes": "score_call_us: one synchronous nemo_score call for one (pos, W) from host "
                         "arrays; fused_step_ms: nemo_optimal_weights for one chain (eval#1 with order "

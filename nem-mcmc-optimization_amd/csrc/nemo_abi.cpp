@@ -1218,7 +1218,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
 }
 
 int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out) {
-  if (n < 0 || fn < 0 || fn > 5 || (n > 0 && (!x || !out || (fn == 3 && !y))))
+  if (n < 0 || fn < 0 || fn > 7 || (n > 0 && (!x || !out || ((fn == 3 || fn == 7) && !y))))
     return fail(NEMO_ERR_ARG, "fn=%d n=%d / null pointer", fn, n);
   if (n == 0) return NEMO_OK;
   int ndev = 0;
@@ -1226,7 +1226,7 @@ int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* 
   double *dx = nullptr, *dy = nullptr, *dout = nullptr;
   HIPCHK(hipMalloc((void**)&dx, (size_t)n * 8));
   HIPCHK(hipMalloc((void**)&dout, (size_t)n * 8));
-  if (fn == 3) HIPCHK(hipMalloc((void**)&dy, (size_t)n * 8));
+  if (fn == 3 || fn == 7) HIPCHK(hipMalloc((void**)&dy, (size_t)n * 8));
   HIPCHK(hipMemcpy(dx, x, (size_t)n * 8, hipMemcpyHostToDevice));
   if (dy) HIPCHK(hipMemcpy(dy, y, (size_t)n * 8, hipMemcpyHostToDevice));
   HIPCHK(nemo::launch_refmath_probe(fn, n, dx, dy, dout, nullptr));

@@ -22,6 +22,10 @@
 #include "nemo_internal.h"
 #include "refmath.h"
 
+// no multiply-add is fused in this file but the explicit fma() calls (HIP's
+// default contraction would fuse them; the functions repeat the pragma)
+#pragma clang fp contract(off)
+
 namespace nemo {
 namespace {
 
@@ -31,7 +35,12 @@ using refmath::LdsTabs;
 struct TabsLds {
   double log_hi[16], log_lo[16], exp_hi[16], exp_lo[16];
   uint64_t gexp[256];
+  uint32_t rbase[64], rin[64];
   __device__ void fill(int t, int nt) {
+    for (int q = t; q < 64; q += nt) {
+      rbase[q] = refmath::kRcp14Base[q];
+      rin[q] = refmath::kRcp14InBucket[q];
+    }
     for (int q = t; q < 16; q += nt) {
       log_hi[q] = refmath::as_double(refmath::kSvmlLogHi[q]);
       log_lo[q] = refmath::as_double(refmath::kSvmlLogLo[q]);
@@ -40,7 +49,7 @@ struct TabsLds {
     }
     for (int q = t; q < 256; q += nt) gexp[q] = refmath::kGlibcExpTab[q];
   }
-  __device__ LdsTabs view() const { return LdsTabs{log_hi, log_lo, exp_hi, exp_lo, gexp}; }
+  __device__ LdsTabs view() const { return LdsTabs{log_hi, log_lo, exp_hi, exp_lo, gexp, rbase, rin}; }
 };
 
 __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nwords, int j, int e) {
@@ -244,6 +253,7 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
   obj.anc = anc[idx];
   // c = a / b, nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k]))
   auto cval = [&](int e) {
+#pragma clang fp contract(off)
     const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
     const double a = (lv - 1.0) * owk[e];
     const double bd = (1.0 - s * a) + s * (lv - 1.0);
@@ -322,7 +332,7 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_generic_k
 }
 
 // device evaluations of refmath.h for the tests (fn: 0 svml_log, 1 svml_exp,
-// 2 expit, 3 logaddexp(x, y), 4 glibc_exp, 5 glibc_log1p)
+// 2 expit, 3 logaddexp(x, y), 4 glibc_exp, 5 glibc_log1p, 6 sqrt, 7 x / y)
 __global__ void refmath_probe_kernel(int fn, int n, const double* __restrict__ x, const double* __restrict__ y,
                                      double* __restrict__ out) {
   __shared__ TabsLds tabs;
@@ -339,7 +349,9 @@ __global__ void refmath_probe_kernel(int fn, int n, const double* __restrict__ x
     case 2: r = refmath::expit(v, tb); break;
     case 3: r = refmath::logaddexp(v, y[g], tb); break;
     case 4: r = refmath::glibc_exp(v, tb); break;
-    default: r = refmath::glibc_log1p(v); break;
+    case 5: r = refmath::glibc_log1p(v); break;
+    case 6: r = __builtin_sqrt(v); break;  // the optimiser's square roots and divisions
+    default: r = v / y[g]; break;
   }
   out[g] = r;
 }

@@ -54,6 +54,7 @@ struct ConstTabs {
   NEMO_RMM double exp_hi(int j) const;
   NEMO_RMM double exp_lo(int j) const;
   NEMO_RMM uint64_t gexp(int i) const;
+  NEMO_RMM int rcp_n(uint32_t p22) const;
 };
 struct LdsTabs {
   const double* log_hi_p;   // [16]
@@ -61,11 +62,18 @@ struct LdsTabs {
   const double* exp_hi_p;   // [16]
   const double* exp_lo_p;   // [16]
   const uint64_t* gexp_p;   // [256]
+  const uint32_t* rbase_p;  // [64] kRcp14Base
+  const uint32_t* rin_p;    // [64] kRcp14InBucket
   NEMO_RMM double log_hi(int j) const { return log_hi_p[j]; }
   NEMO_RMM double log_lo(int j) const { return log_lo_p[j]; }
   NEMO_RMM double exp_hi(int j) const { return exp_hi_p[j]; }
   NEMO_RMM double exp_lo(int j) const { return exp_lo_p[j]; }
   NEMO_RMM uint64_t gexp(int i) const { return gexp_p[i]; }
+  // the bucketed form of the step function (equal for every prefix: tests)
+  NEMO_RMM int rcp_n(uint32_t p22) const {
+    const uint32_t b = p22 >> 16;
+    return (int)rbase_p[b] + (p22 >= rin_p[b] ? 1 : 0);
+  }
 };
 NEMO_RM uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
 NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
@@ -74,6 +82,11 @@ NEMO_RMM double ConstTabs::log_lo(int j) const { return as_double(kSvmlLogLo[j])
 NEMO_RMM double ConstTabs::exp_hi(int j) const { return as_double(kSvmlExpHi[j]); }
 NEMO_RMM double ConstTabs::exp_lo(int j) const { return as_double(kSvmlExpLo[j]); }
 NEMO_RMM uint64_t ConstTabs::gexp(int i) const { return kGlibcExpTab[i]; }
+NEMO_RMM int ConstTabs::rcp_n(uint32_t p22) const {
+  int n = 0;
+  for (int t = 0; t < 16; ++t) n += p22 >= kRcp14Switch[t] ? 1 : 0;
+  return n;
+}
 
 // ---------------------------------------------------------------------------
 // glibc 2.35 exp (sysdeps/ieee754/dbl-64/e_exp.c, Szabolcs Nagy's table
@@ -255,9 +268,7 @@ NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   const double m = as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
   double k = (double)((int)((b >> 52) & 0x7ff) - 1023);
   const uint32_t p22 = (uint32_t)(b >> 30) & 0x3fffff;
-  int n = 0;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) n += p22 >= kRcp14Switch[t] ? 1 : 0;
+  const int n = tb.rcp_n(p22);
   const double r = (double)(32 - n) * 0.03125;
   const double R = fma_(r, m, -1.0);
   if (r < 0.75) k = k + 1.0;

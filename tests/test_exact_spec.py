@@ -64,6 +64,23 @@ def test_refmath_host_check_against_the_libraries(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_rcp14_step_function_bucketed_form_is_the_same():
+    """svml_log's reduction point r = RNE_1/32(vrcp14pd(m)): the device's
+    bucketed lookup (kRcp14Base / kRcp14InBucket) gives the threshold count
+    of kRcp14Switch for every one of the 2^22 mantissa prefixes."""
+    import re
+    text = open(os.path.join(CSRC, "refmath_tables.h")).read()
+
+    def arr(name):
+        body = re.search(name + r"\[\d+\] = \{([^}]*)\}", text).group(1)
+        return np.array([int(v.strip().rstrip("u"), 0) for v in body.split(",") if v.strip()], dtype=np.int64)
+    th, base, inb = arr("kRcp14Switch"), arr("kRcp14Base"), arr("kRcp14InBucket")
+    p = np.arange(1 << 22, dtype=np.int64)
+    n_loop = np.searchsorted(th, p, side="right")
+    n_bucket = base[p >> 16] + (p >= inb[p >> 16])
+    assert np.array_equal(n_loop, n_bucket)
+
+
 def test_elementwise_functions_equal_numpy_scipy(spec):
     rng = np.random.default_rng(3)
     n = 200000

@@ -44,6 +44,11 @@ def test_refmath_on_the_device_equals_numpy_scipy_glibc():
     assert _bits_equal(_lib.refmath_probe("glibc_exp", x), [math.exp(v) for v in x])
     x = np.exp(rng.uniform(np.log(1e-300), 0, 1 << 16))
     assert _bits_equal(_lib.refmath_probe("glibc_log1p", x), [math.log1p(v) for v in x])
+    # the IEEE operations the optimiser's control needs correctly rounded
+    x = np.exp(rng.uniform(-700, 700, n))
+    assert _bits_equal(_lib.refmath_probe("sqrt", x), np.sqrt(x))
+    y = rng.normal(size=n) * np.exp(rng.uniform(-300, 300, n))
+    assert _bits_equal(_lib.refmath_probe("div", x, y), x / y)
 
 
 @pytest.mark.parametrize("name", ["net2_200", "C2_20"])

@@ -127,6 +127,13 @@ def main():
     loghi, loglo = lanes(lg, 0) + lanes(lg, 0x40), lanes(lg, 0x80) + lanes(lg, 0xc0)
     exphi, explo = lanes(ex, 0) + lanes(ex, 0x40), lanes(ex, 0x80) + lanes(ex, 0xc0)
     th = rcp14_thresholds()
+    # the same step function by 64 buckets of the 22-bit prefix (p >> 16):
+    # the thresholds are more than 2^16 apart, so a bucket holds at most one
+    assert all(b - a > (1 << 16) for a, b in zip(th, th[1:])) and th[0] > 0
+    base = [sum(1 for t in th if t < (bk << 16)) for bk in range(64)]
+    inb = [next((t for t in th if (t >> 16) == bk), 0xFFFFFFFF) for bk in range(64)]
+    for p in range(0, 1 << 22, 977):   # spot check here; tests check every prefix
+        assert base[p >> 16] + (p >= inb[p >> 16]) == sum(1 for t in th if p >= t)
     import numpy
     text = f"""// GENERATED by tools/gen_refmath_tables.py -- do not edit.
 // Data of the libraries the reference's arithmetic runs in (glibc 2.35 libm,
@@ -165,6 +172,13 @@ constexpr uint64_t kSvmlExpLo[16] = {{
 // instruction; monotone)
 constexpr uint32_t kRcp14Switch[16] = {{
     {", ".join(str(v) for v in th)}
+}};
+// ... and by bucket p >> 16: n = kRcp14Base[b] + (p >= kRcp14InBucket[b])
+constexpr uint32_t kRcp14Base[64] = {{
+    {", ".join(str(v) for v in base)}
+}};
+constexpr uint32_t kRcp14InBucket[64] = {{
+    {", ".join(f"0x{v:x}u" for v in inb)}
 }};
 
 }}  // namespace refmath
