@@ -164,6 +164,7 @@ def test_local_opt_vs_scipy_records(name, prod):
     z = golden(f"localopt_{name}.npz")
     e = z["c"].shape[1]
     eng = Engine(np.zeros((3, e)), np.zeros((2, 2, e)))
+    eng.set_option("exact", 0)   # the fast objective (test_gpu_exact.py: the exact one, bit for bit)
     eng.set_option("local_prod", prod)
     xs, fs, nit, nfev, st = eng.local_opt(z["c"], z["anc"], z["x0"])
     assert np.all(st <= 1)
@@ -184,9 +185,12 @@ def _oracle_step_inputs(u, t, perm, w_raw):
 
 
 def test_fused_step_vs_oracle_c3(c3_model):
-    """One get_optimal_weights at 64x2000 (2016 local optima) vs the oracle."""
+    """One get_optimal_weights at 64x2000 (2016 local optima) vs the oracle,
+    with the fast kernels (option exact = 0; the default exact arithmetic:
+    test_gpu_exact.py, every weight to the bit)."""
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m, eng = c3_model
+    eng.set_option("exact", 0)
     t = m.get_score_tensor()
     rng = np.random.default_rng(12)
     perm = rng.permutation(m.num_s)
@@ -207,6 +211,7 @@ def test_fused_step_vs_oracle_c3(c3_model):
     assert int((dw > 1e-6).sum()) <= 16 and dw.max() <= 1e-2
     assert np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
     assert abs(got_dag - ref_dag) <= LL_TOL
+    eng.set_option("exact", 1)
 
 
 def _run_sampler(m, order, gamma, swap_prob, n, state):
@@ -226,10 +231,13 @@ def test_trajectory_net2_200(net2):
                              int(z["n_iter"]), state)
     assert np.array_equal(np.array(smp.accepted), z["acc"])
     scores = np.array(smp.all_score_list)
-    assert np.max(np.abs(scores - z["all_scores"])) <= LL_TOL
-    assert abs(best - float(z["best_score"])) <= LL_TOL
+    # the reference's arithmetic (option exact, the default): every score,
+    # the best score and the final weights to the bit
+    assert np.array_equal(scores, z["all_scores"])
+    assert best == float(z["best_score"])
     assert np.array_equal(smp.best_order, z["best_order"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    assert np.array_equal(smp.parent_weights, z["final_W"])
 
 
 def test_trajectory_net2_use_nem_50(net2):
@@ -248,12 +256,12 @@ def test_trajectory_net2_use_nem_50(net2):
     best, best_dag = smp.method(n_iterations=int(z["n_iter"]), gamma=float(z["gamma"]),
                                 swap_prob=float(z["swap_prob"]), verbose=False, use_nem=True)
     assert np.array_equal(np.array(smp.accepted), z["acc"])
-    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
-    assert abs(best - float(z["best_score"])) <= LL_TOL
+    assert np.array_equal(np.array(smp.all_score_list), z["all_scores"])
+    assert best == float(z["best_score"])
     assert np.array_equal(smp.best_order, z["best_order"])
     assert np.array_equal(np.asarray(best_dag), z["best_dag"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
-    assert np.max(np.abs(smp.parent_weights - z["final_W"])) <= 1e-6
+    assert np.array_equal(smp.parent_weights, z["final_W"])
 
 
 def test_trajectory_c2_20():
@@ -263,37 +271,30 @@ def test_trajectory_c2_20():
     smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
                              int(z["n_iter"]), state)
     assert np.array_equal(np.array(smp.accepted), z["acc"])
-    assert np.max(np.abs(np.array(smp.all_score_list) - z["all_scores"])) <= LL_TOL
+    assert np.array_equal(np.array(smp.all_score_list), z["all_scores"])
+    assert np.array_equal(smp.parent_weights, z["final_W"])
 
 
-# steps whose score may leave 1e-6 of the reference's: at C3 a few of each
-# step's 2016 local optima land within the forward-difference noise (h = 1e-8)
-# of scipy's, and a weight that sits at 0.5 can binarise to the other side
-# (DESIGN.md 3.5); over the 100-step run that happens once (step 27, then the
-# chains re-align: the accepted moves, best order and random state stay equal)
-@pytest.mark.parametrize("n,max_off", [(20, 0), (100, 1)])
-def test_trajectory_c3(n, max_off):
+@pytest.mark.parametrize("n", [20, 100])
+def test_trajectory_c3(n):
     """C3, the headline model (64 x 2000): n steps of the reference's method()
-    with its seed (tests/golden/make_goldens.py --only-traj-c3 n): identical
-    proposals and accepted moves, scores within 1e-6 (all but max_off steps),
-    the same best score and order, the same final random state, and final
-    weights (every step's 2016 local optima carried into the next) within
-    1e-2 and binarised the same.""" 
+    with its seed (tests/golden/make_goldens.py --only-traj-c3 n), in the
+    reference's own arithmetic (option exact, the default): identical
+    proposals and accepted moves, and every score, the best score and order,
+    the final random state and the final weights (every step's 2016 local
+    optima carried into the next) equal to the reference's to the bit."""
     z = golden(f"traj_C3_{n}.npz")
     m = generator.synthetic_nem(64, 2000, 0)
     state = random.getstate()
     smp, best = _run_sampler(m, z["order0"], float(z["gamma"]), float(z["swap_prob"]),
                              int(z["n_iter"]), state)
     assert np.array_equal(np.array(smp.accepted), z["acc"])
-    d = np.abs(np.array(smp.all_score_list) - z["all_scores"])
-    assert int((d > LL_TOL).sum()) <= max_off, np.where(d > LL_TOL)[0].tolist()
-    assert abs(best - float(z["best_score"])) <= LL_TOL
+    d = np.array(smp.all_score_list) != z["all_scores"]
+    assert not d.any(), np.where(d)[0].tolist()
+    assert best == float(z["best_score"])
     assert np.array_equal(smp.best_order, z["best_order"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
-    assert np.array_equal(smp.parent_weights > 0.5, z["final_W"] > 0.5)
-    # a few optima per step follow another line-search path than scipy's
-    # (test_fused_step_vs_oracle_c3: up to ~1e-2 in the weight, never across 0.5)
-    assert np.max(np.abs(smp.parent_weights - z["final_W"])) <= 1e-2
+    assert np.array_equal(smp.parent_weights, z["final_W"])
 
 
 def _record_sampler(smp):
@@ -326,9 +327,8 @@ def test_trajectory_c3_until_the_reference_raises():
     run ends in step 128, when one of that step's local optimisations
     terminates abnormally and method() raises (nem_order_mcmc.py:168-169;
     make_goldens.py --only-traj-c3 500).  The mirror makes the same 128
-    proposals and 127 accept decisions, scores every completed step within
-    1e-6 of the reference but at the steps counted below, and raises in the
-    same step."""
+    proposals and 127 accept decisions, scores every completed step to the
+    bit, and raises in the same step with the same weights."""
     from nemo.nem_order_mcmc import NEMOrderMCMC
     z = golden("traj_C3_500.npz")
     m = generator.synthetic_nem(64, 2000, 0)
@@ -340,15 +340,11 @@ def test_trajectory_c3_until_the_reference_raises():
     assert len(rec["perm"]) == int(z["raised_in_step"])
     assert np.array_equal(np.array(rec["perm"]), z["perm"])
     assert np.array_equal(np.array(rec["acc"]), z["acc"])
-    d = np.abs(np.array(rec["scores"][1:1 + int(z["steps_completed"])]) - z["step_scores"])
-    off = np.where(d > LL_TOL)[0].tolist()
-    print("C3 steps off by more than 1e-6:", off, "max", float(d.max()))
-    assert len(off) <= C3_STEPS_OFF, off
-
-
-# completed C3 steps (of 127) whose score may leave 1e-6 of the reference's
-# (DESIGN.md 3.5): measured on the GPU, asserted exactly
-C3_STEPS_OFF = 1
+    got = np.array(rec["scores"][1:1 + int(z["steps_completed"])])
+    off = np.where(got != z["step_scores"])[0].tolist()
+    print("C3 steps whose score differs from the reference's:", off)
+    assert not off, off
+    assert np.array_equal(smp.parent_weights, z["W_at_raise"])
 
 
 def test_edge_cases():
