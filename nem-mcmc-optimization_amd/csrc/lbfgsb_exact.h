@@ -80,16 +80,42 @@ NEMO_LB double ob_ddot(int n, const double* x, const double* y) {
   return dot;
 }
 
-// OpenBLAS dgemv_t_SKYLAKEX with alpha = -1: y[k * incy] += -(A(:, k)' x),
-// A m x n column-major (lda), m < 2048
-NEMO_LB void ob_gemv_t_m1(int m, int n, const double* a, int lda, const double* x, double* y, int incy) {
+// The control's wave: every lane runs the optimiser (uniform values, scalar
+// branches); the independent entries of its small matrices are spread over
+// the lanes -- each entry computed by one lane, in the library's order -- and
+// written to `mem` (LDS), and the wave syncs before they are read.  On the
+// host: one lane, the loops in sequence.
+struct Lanes {
+  int id, n;
+};
+NEMO_LB Lanes lanes() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return Lanes{(int)__lane_id(), 64};
+#else
+  return Lanes{0, 1};
+#endif
+}
+NEMO_LB void lanes_sync() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
+// One output of OpenBLAS dgemv_t_SKYLAKEX with alpha = -1 (A m x n
+// column-major, lda, m < 2048): y - A(:, c)' x for column c, in the order of
+// the kernel that column falls to -- dgemv_kernel_4x4 (per-column FMA lanes
+// summed (0+2)+(1+3)) for the first 4 (n / 4) columns, then the unfused
+// 2-lane dgemv_kernel_4x2, then dgemv_kernel_4x1 -- and the m % 4 tail rows
+// last with x pre-scaled by alpha.
+NEMO_LB double ob_gemv_t_m1_col(int m, int n, int c, const double* a, int lda, const double* x, double y) {
 #pragma clang fp contract(off)
   const int m3 = m & 3, nb = m - m3;
-  int c = 0;
+  const double* col = a + (long)c * lda;
   if (nb > 0) {
-    const int n1 = n >> 2, n2 = n & 3;
-    for (int g = 0; g < n1 * 4; ++g, ++c) {  // dgemv_kernel_4x4: per-column FMA lanes
-      const double* col = a + (long)c * lda;
+    const int n4 = (n >> 2) * 4, n2 = n & 3;
+    if (c < n4) {
       double acc[4] = {0, 0, 0, 0};
       int i = 0;
       if (nb & 4) {
@@ -101,23 +127,17 @@ NEMO_LB void ob_gemv_t_m1(int m, int n, const double* a, int lda, const double* 
         for (int l = 0; l < 4; ++l) acc[l] = fma_(x[i + 4 + l], col[i + 4 + l], acc[l]);
       }
       const double t = (acc[0] + acc[2]) + (acc[1] + acc[3]);
-      y[c * incy] = fma_(t, -1.0, y[c * incy]);  // add_y (exact for alpha = -1 either way)
-    }
-    if (n2 & 2) {  // dgemv_kernel_4x2: unfused 2-lane sums
-      for (int q = 0; q < 2; ++q, ++c) {
-        const double* col = a + (long)c * lda;
-        double acc0 = 0.0, acc1 = 0.0;
-        for (int i = 0; i < nb; i += 4) {
-          acc0 = acc0 + x[i] * col[i];
-          acc1 = acc1 + x[i + 1] * col[i + 1];
-          acc0 = acc0 + x[i + 2] * col[i + 2];
-          acc1 = acc1 + x[i + 3] * col[i + 3];
-        }
-        y[c * incy] = fma_(acc0 + acc1, -1.0, y[c * incy]);
+      y = fma_(t, -1.0, y);  // add_y (exact for alpha = -1 either way)
+    } else if ((n2 & 2) && c < n4 + 2) {
+      double acc0 = 0.0, acc1 = 0.0;
+      for (int i = 0; i < nb; i += 4) {
+        acc0 = acc0 + x[i] * col[i];
+        acc1 = acc1 + x[i + 1] * col[i + 1];
+        acc0 = acc0 + x[i + 2] * col[i + 2];
+        acc1 = acc1 + x[i + 3] * col[i + 3];
       }
-    }
-    if (n2 & 1) {  // dgemv_kernel_4x1: two 2-lane accumulators
-      const double* col = a + (long)c * lda;
+      y = fma_(acc0 + acc1, -1.0, y);
+    } else {
       double p0 = 0.0, p1 = 0.0, q0 = 0.0, q1 = 0.0;
       for (int i = 0; i < nb; i += 4) {
         p0 = p0 + col[i] * x[i];
@@ -125,28 +145,27 @@ NEMO_LB void ob_gemv_t_m1(int m, int n, const double* a, int lda, const double* 
         q0 = q0 + col[i + 2] * x[i + 2];
         q1 = q1 + col[i + 3] * x[i + 3];
       }
-      y[c * incy] = fma_((p0 + q0) + (p1 + q1), -1.0, y[c * incy]);
-      ++c;
+      y = fma_((p0 + q0) + (p1 + q1), -1.0, y);
     }
   }
   if (m3) {  // the last m3 rows, x pre-scaled by alpha
     const int r = nb;
     const double xt0 = -x[r], xt1 = m3 > 1 ? -x[r + 1] : 0.0, xt2 = m3 > 2 ? -x[r + 2] : 0.0;
-    for (int k = 0; k < n; ++k) {
-      const double* col = a + (long)k * lda + r;
-      if (m3 == 1) {
-        y[k * incy] = fma_(col[0], xt0, y[k * incy]);
-      } else {
-        double t = fma_(col[0], xt0, col[1] * xt1);
-        if (m3 == 3) t = fma_(col[2], xt2, t);
-        y[k * incy] = t + y[k * incy];
-      }
+    const double* cr = col + r;
+    if (m3 == 1) {
+      y = fma_(cr[0], xt0, y);
+    } else {
+      double t = fma_(cr[0], xt0, cr[1] * xt1);
+      if (m3 == 3) t = fma_(cr[2], xt2, t);
+      y = t + y;
     }
   }
+  return y;
 }
 
-// OpenBLAS dpotrf('U') for n <= 16 (potf2_U); returns info (0 or j + 1)
-NEMO_LB int ob_potrf_u(int n, double* a, int lda) {
+// OpenBLAS dpotrf('U') for n <= 16 (potf2_U); returns info (0 or j + 1).
+// Row j's update (dgemv_t) and scaling by 1 / ajj: one column per lane.
+NEMO_LB int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 #pragma clang fp contract(off)
   for (int j = 0; j < n; ++j) {
     double* cj = a + (long)j * lda;
@@ -159,9 +178,14 @@ NEMO_LB int ob_potrf_u(int n, double* a, int lda) {
     cj[j] = ajj;
     const int i = n - j - 1;
     if (i > 0) {
-      if (j > 0) ob_gemv_t_m1(j, i, a + (long)(j + 1) * lda, lda, cj, cj + j + lda, lda);
       const double inv = 1.0 / ajj;
-      for (int k = 0; k < i; ++k) cj[j + (long)(k + 1) * lda] = cj[j + (long)(k + 1) * lda] * inv;
+      for (int k = L.id; k < i; k += L.n) {
+        double* y = cj + j + (long)(k + 1) * lda;
+        double v = *y;
+        if (j > 0) v = ob_gemv_t_m1_col(j, i, k, a + (long)(j + 1) * lda, lda, cj, v);
+        *y = v * inv;
+      }
+      lanes_sync();
     }
   }
   return 0;
@@ -196,12 +220,13 @@ NEMO_LB int ob_trsv_nun(int n, const double* u, int ldu, double* b) {
 }
 
 // dtrtrs('U', 'T', 'N') with nrhs >= 2 (trsm_LTUN: the inverted diagonal,
-// row blocks of 16 then 8, 4, 2, 1), n <= 16, B n x nrhs (ldb)
-NEMO_LB int ob_trsm_lt(int n, int nrhs, const double* u, int ldu, double* b, int ldb) {
+// row blocks of 16 then 8, 4, 2, 1), n <= 16, B n x nrhs (ldb); one
+// right-hand side per lane
+NEMO_LB int ob_trsm_lt(int n, int nrhs, const double* u, int ldu, double* b, int ldb, Lanes L) {
 #pragma clang fp contract(off)
   for (int i = 0; i < n; ++i)
     if (uni(u[i + (long)i * ldu] == 0.0)) return i + 1;
-  for (int j = 0; j < nrhs; ++j) {
+  for (int j = L.id; j < nrhs; j += L.n) {
     double* x = b + (long)j * ldb;
     int r0 = 0;
     for (int sz = 16; sz >= 1; sz >>= 1) {
@@ -221,6 +246,7 @@ NEMO_LB int ob_trsm_lt(int n, int nrhs, const double* u, int ldu, double* b, int
       r0 += sz;
     }
   }
+  lanes_sync();
   return 0;
 }
 
@@ -228,78 +254,115 @@ NEMO_LB int ob_trsm_lt(int n, int nrhs, const double* u, int ldu, double* b, int
 NEMO_LB double prod0(double a, double b) { return fma_(a, b, 0.0); }   // ddot, n = 1
 NEMO_LB double sum0(double a, double b) { return 0.0 + a * b; }        // C loop from zero
 
+// The s / y memory in logical order (0 = the oldest pair): the library's
+// circular buffer (head, itail) holds the same pairs, and every product reads
+// them by logical index, so the bits do not depend on where they are stored.
+// When the memory is full the oldest pair is dropped by shifting.
 struct Ring {
-  int col = 0, head = 0, itail = 0, iupdat = 0;
-  NEMO_LB int p(int i) const { return (head + i) % kM; }   // logical i (0 = oldest) -> slot
+  int col = 0, iupdat = 0;
 };
 
-// formt: T = theta SS + L D^-1 L' and its Cholesky factor; returns info
-NEMO_LB int formt(Mem& mem, const Ring& rg, double theta) {
+// matupd: the new pair (s, y, s's, s'y) as the newest
+NEMO_LB void matupd(Mem& mem, Ring& rg, double s, double y, double ssd, double syd) {
+  rg.iupdat += 1;
+  if (rg.iupdat <= kM) {
+    rg.col = rg.iupdat;
+  } else {
+    for (int i = 0; i + 1 < kM; ++i) {
+      mem.ws(i) = mem.ws(i + 1);
+      mem.wy(i) = mem.wy(i + 1);
+      mem.ssd(i) = mem.ssd(i + 1);
+      mem.syd(i) = mem.syd(i + 1);
+    }
+  }
+  const int t = rg.col - 1;
+  mem.ws(t) = s;
+  mem.wy(t) = y;
+  mem.ssd(t) = ssd;
+  mem.syd(t) = syd;
+}
+
+// formt: T = theta SS + L D^-1 L' and its Cholesky factor; returns info.
+// T's upper triangle: one entry per lane.
+NEMO_LB int formt(Mem& mem, const Ring& rg, double theta, Lanes L) {
 #pragma clang fp contract(off)
   const int col = rg.col;
   double* wt = mem.wt();
-  auto sy = [&](int i, int k) { return i == k ? mem.syd(rg.p(i)) : prod0(mem.ws(rg.p(i)), mem.wy(rg.p(k))); };
-  auto ss = [&](int i, int k) { return i == k ? mem.ssd(rg.p(i)) : prod0(mem.ws(rg.p(i)), mem.ws(rg.p(k))); };
-  for (int j = 0; j < col; ++j) wt[(long)j * kLdT] = theta * ss(0, j);
-  for (int i = 1; i < col; ++i)
-    for (int j = i; j < col; ++j) {
-      const int k1 = i < j ? i : j;
+  auto sy = [&](int i, int k) { return i == k ? mem.syd(i) : prod0(mem.ws(i), mem.wy(k)); };
+  auto ss = [&](int i, int k) { return i == k ? mem.ssd(i) : prod0(mem.ws(i), mem.ws(k)); };
+  for (int t = L.id; t < kM * kM; t += L.n) {
+    const int i = t % kM, j = t / kM;
+    if (j >= col || i > j) continue;
+    if (i == 0) {
+      wt[(long)j * kLdT] = theta * ss(0, j);
+    } else {
       double ddum = 0.0;
-      for (int k = 0; k < k1; ++k) ddum = ddum + sy(i, k) * sy(j, k) / sy(k, k);
+      for (int k = 0; k < i; ++k) ddum = ddum + sy(i, k) * sy(j, k) / sy(k, k);
       wt[i + (long)j * kLdT] = ddum + theta * ss(i, j);
     }
-  return ob_potrf_u(col, wt, kLdT);
+  }
+  lanes_sync();
+  return ob_potrf_u(col, wt, kLdT, L);
 }
 
 // formk for n = nsub = 1, the variable free and staying free: WN (upper,
-// 2col x 2col, ld 2m) and its two Cholesky factorisations; info 0, -1, -2
-NEMO_LB int formk(Mem& mem, const Ring& rg, double theta) {
+// 2col x 2col, ld 2m) and its two Cholesky factorisations; info 0, -1, -2.
+// WN's entries, the solve's right-hand sides and the (2,2) block's updates:
+// one per lane.
+NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
 #pragma clang fp contract(off)
-  const int col = rg.col;
+  const int col = rg.col, c2 = 2 * col;
   double* wn = mem.wn();
   auto at = [&](int r, int c) -> double& { return wn[r + (long)c * kLdN]; };
-  for (int iy = 0; iy < col; ++iy) {
-    const int is = col + iy;
-    const double yi = mem.wy(rg.p(iy)), si = mem.ws(rg.p(iy));
-    for (int jy = 0; jy <= iy; ++jy) {
-      at(jy, iy) = sum0(yi, mem.wy(rg.p(jy))) / theta;   // Y'ZZ'Y / theta
-      at(col + jy, is) = 0.0 * theta;                     // S'AA'S theta (no active set)
+  for (int t = L.id; t < kLdN * kLdN; t += L.n) {
+    const int r = t % kLdN, c = t / kLdN;
+    if (c >= c2 || r > c) continue;
+    double v;
+    if (c < col) {            // Y'ZZ'Y / theta, + s'y on the diagonal
+      v = sum0(mem.wy(c), mem.wy(r)) / theta;
+      if (r == c) v = v + mem.syd(c);
+    } else if (r < col) {     // -L_a (zero: no active set) and R_z
+      const int iy = c - col;
+      v = r < iy ? -0.0 : sum0(mem.ws(iy), mem.wy(r));
+    } else {                  // S'AA'S theta (no active set)
+      v = 0.0 * theta;
     }
-    for (int jy = 0; jy < iy; ++jy) at(jy, is) = -0.0;   // -L_a
-    for (int jy = iy; jy < col; ++jy) at(jy, is) = sum0(si, mem.wy(rg.p(jy)));   // R_z
-    at(iy, iy) = at(iy, iy) + mem.syd(rg.p(iy));
+    at(r, c) = v;
   }
-  if (ob_potrf_u(col, wn, kLdN) != 0) return -1;
+  lanes_sync();
+  if (ob_potrf_u(col, wn, kLdN, L) != 0) return -1;
   // L^-1 (-L_a' + R_z') in the (1,2) block: one dtrtrs call with nrhs = col
   double* b12 = wn + (long)col * kLdN;
-  const int info = col == 1 ? ob_trsv_tun(1, wn, kLdN, b12) : ob_trsm_lt(col, col, wn, kLdN, b12, kLdN);
+  const int info = col == 1 ? ob_trsv_tun(1, wn, kLdN, b12) : ob_trsm_lt(col, col, wn, kLdN, b12, kLdN, L);
   if (info != 0) return -1;
-  for (int is = col; is < 2 * col; ++is)
-    for (int js = is; js < 2 * col; ++js)
-      at(is, js) = at(is, js) + ob_ddot(col, wn + (long)is * kLdN, wn + (long)js * kLdN);
-  if (ob_potrf_u(col, wn + col + (long)col * kLdN, kLdN) != 0) return -2;
+  for (int t = L.id; t < kM * kM; t += L.n) {
+    const int a = t % kM, b = t / kM;
+    if (b >= col || a > b) continue;
+    const int is = col + a, js = col + b;
+    at(is, js) = at(is, js) + ob_ddot(col, wn + (long)is * kLdN, wn + (long)js * kLdN);
+  }
+  lanes_sync();
+  if (ob_potrf_u(col, wn + col + (long)col * kLdN, kLdN, L) != 0) return -2;
   return 0;
 }
 
 // subsm from z = x with r = -g (cmprlb, unconstrained): the Newton step;
 // false when a triangular solve is singular (the caller restarts)
-NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z) {
+NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z, Lanes L) {
 #pragma clang fp contract(off)
   const int col = rg.col, c2 = 2 * col;
   double* wv = mem.wv();   // (a local array would live in per-lane scratch on the device)
-  for (int i = 0; i < col; ++i) {
-    wv[i] = sum0(mem.wy(rg.p(i)), r);
-    wv[col + i] = theta * sum0(mem.ws(rg.p(i)), r);
+  for (int i = L.id; i < col; i += L.n) {
+    wv[i] = sum0(mem.wy(i), r);
+    wv[col + i] = theta * sum0(mem.ws(i), r);
   }
+  lanes_sync();
   const double* wn = mem.wn();
   if (ob_trsv_tun(c2, wn, kLdN, wv) != 0) return false;
   for (int i = 0; i < col; ++i) wv[i] = -wv[i];
   if (ob_trsv_nun(c2, wn, kLdN, wv) != 0) return false;
   double d = r;
-  for (int jy = 0; jy < col; ++jy) {
-    const int p = rg.p(jy);
-    d = d + mem.wy(p) * wv[jy] / theta + mem.ws(p) * wv[col + jy];
-  }
+  for (int jy = 0; jy < col; ++jy) d = d + mem.wy(jy) * wv[jy] / theta + mem.ws(jy) * wv[col + jy];
   d = d * (1.0 / theta);
   z = x + d;   // the projection step of L-BFGS-B 3.0 (no bounds: alpha = 1, same bits)
   return true;
@@ -307,101 +370,133 @@ NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, d
 
 }  // namespace lbx
 
-// Minimise the reference's unbounded 1-D objective from x0 with scipy's
-// exact arithmetic (header); fg as lbfgsb1_minimize.  Status as there.
-template <class FG>
-NEMO_LB LbfgsResult lbfgsb1_minimize_exact(FG& fg, double x0, lbx::Mem mem) {
+// (tools/ubench/exact_obj.hip times the parts of the control through this
+// hook; in the library it is the statement itself)
+#ifndef NEMO_LBX_T
+#define NEMO_LBX_T(k, stmt) stmt
+#endif
+
+// The optimiser as a resumable machine ("reverse communication", as the
+// Fortran original): lbx_run advances to the next evaluation the library
+// would make (or to the end), the caller evaluates the objective at the two
+// points of the forward difference and hands the values to lbx_feed.  On the
+// device the whole state lives in LDS next to `mem`, so the objective's
+// registers and the optimiser's never overlap.
+struct LbxState {
+  double theta, x, f, g, z, d, stp, xk, fold, gold, gdold, dtd;
+  double x_eval, x1, x_last, f_last, g_last;
+  lb::Dcsrch ls;
+  lbx::Ring rg;
+  int nfev, nit, ifun, status;
+  bool in_ls, updatd, have_last;
+};
+
+NEMO_LB void lbx_init(LbxState& S, double x0) {
+  S.theta = 1.0;
+  S.x = x0; S.f = 0.0; S.g = 0.0;
+  S.z = S.d = S.stp = S.xk = S.fold = S.gold = S.gdold = S.dtd = 0.0;
+  S.x_eval = x0; S.x1 = x0;
+  S.x_last = S.f_last = S.g_last = 0.0;
+  S.ls = lb::Dcsrch{};
+  S.rg = lbx::Ring{};
+  S.nfev = S.nit = S.ifun = 0;
+  S.status = -1;
+  S.in_ls = S.updatd = S.have_last = false;
+}
+
+// scipy's ScalarFunction: f at x_eval and the forward difference at x1
+NEMO_LB void lbx_feed(LbxState& S, double f0, double f1) {
+#pragma clang fp contract(off)
+  S.nfev += 2;
+  S.f_last = f0;
+  S.g_last = (f1 - f0) / (S.x1 - S.x_eval);
+  S.have_last = true;
+  S.x_last = S.x_eval;
+}
+
+// true: evaluate at (S.x_eval, S.x1) and lbx_feed; false: done, the result
+// in S.x, S.f, S.nit, S.nfev, S.status
+NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
 #pragma clang fp contract(off)
   using namespace lb;
   using lbx::fma_;
   const double tol = (0.01 / kEpsMch) * kEpsMch;
   const double pgtol = 0.01;
   const int maxls = 20, maxiter = 15000, maxfun = 15000;
-  int nfev = 0, nit = 0, ifun = 0;
-  bool in_ls = false, updatd = false;
-  lbx::Ring rg;
-  double theta = 1.0;
-  double x = x0, f = 0.0, g = 0.0;
-  double z = 0.0, d = 0.0, stp = 0.0, xk = 0.0, fold = 0.0, gold = 0.0, gdold = 0.0, dtd = 0.0;
-  double x_eval = x0;
-  bool have_last = false;
-  double x_last = 0.0, f_last = 0.0, g_last = 0.0;
-  Dcsrch ls;
+  const lbx::Lanes L = lbx::lanes();
   auto restart = [&]() {
-    rg = lbx::Ring{};
-    theta = 1.0;
-    updatd = false;
+    S.rg = lbx::Ring{};
+    S.theta = 1.0;
+    S.updatd = false;
+  };
+  auto done = [&](double x, double f, int status) {
+    S.x = x; S.f = f; S.status = status;
+    return false;
   };
   for (;;) {
-    // ---- the single evaluation site (scipy's ScalarFunction memoises the
-    // last point: a repeated x costs no evaluation)
-    if (uni(!(have_last && x_eval == x_last))) {
+    // ---- the single evaluation site (the ScalarFunction memoises the last
+    // point: a repeated x costs no evaluation)
+    if (uni(!(S.have_last && S.x_eval == S.x_last))) {
+      const double xe = S.x_eval;
       double h = 1e-8;
-      if (uni((x_eval + h) - x_eval == 0.0))
-        h = kSqrtEps * (x_eval >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(x_eval));
-      const double x1 = x_eval + h;
-      double f0, f1;
-      fg(x_eval, x1, f0, f1);
-      nfev += 2;
-      f_last = f0;
-      g_last = (f1 - f0) / (x1 - x_eval);
-      have_last = true;
-      x_last = x_eval;
+      if (uni((xe + h) - xe == 0.0)) h = kSqrtEps * (xe >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(xe));
+      S.x1 = xe + h;
+      return true;
     }
-    x = x_eval;
-    f = f_last;
-    g = g_last;
-    if (uni(!in_ls)) {
-      if (uni(fabs(g) <= pgtol)) return LbfgsResult{x, f, 0, nfev, 0};
+    double x = S.x_eval, f = S.f_last, g = S.g_last;
+    if (uni(!S.in_ls)) {
+      if (uni(fabs(g) <= pgtol)) { S.nit = 0; return done(x, f, 0); }
     } else {
-      int task = ls.step(stp, f, lbx::prod0(g, d));
+      double stp = S.stp;
+      int task;
+      NEMO_LBX_T(0, task = S.ls.step(stp, f, lbx::prod0(g, S.d)));
+      S.stp = stp;
       if (uni(task == 0)) {
-        ++ifun;
-        if (uni(ifun - 1 < maxls)) {
-          x_eval = (stp == 1.0) ? z : stp * d + xk;
+        ++S.ifun;
+        if (uni(S.ifun - 1 < maxls)) {
+          S.x_eval = (stp == 1.0) ? S.z : stp * S.d + S.xk;
           continue;
         }
         task = -1;
       }
       if (uni(task < 0)) {  // line search failed: previous iterate, restart or give up
-        x = xk; f = fold; g = gold;
-        if (uni(rg.col == 0)) return LbfgsResult{x, f, nit, nfev, 2};
+        x = S.xk; f = S.fold; g = S.gold;
+        if (uni(S.rg.col == 0)) return done(x, f, 2);
         restart();
       } else {
-        ++nit;
-        if (uni(fabs(g) <= pgtol)) return LbfgsResult{x, f, nit, nfev, 0};
-        if (uni((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))) return LbfgsResult{x, f, nit, nfev, 1};
-        if (uni(nit >= maxiter || nfev > maxfun)) return LbfgsResult{x, f, nit, nfev, 3};
+        ++S.nit;
+        if (uni(fabs(g) <= pgtol)) return done(x, f, 0);
+        const double fold = S.fold;
+        if (uni((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))) return done(x, f, 1);
+        if (uni(S.nit >= maxiter || S.nfev > maxfun)) return done(x, f, 3);
+        double d = S.d;
+        const double gdold = S.gdold;
         const double gd = lbx::prod0(g, d);
-        const double r = g - gold;
+        const double r = g - S.gold;
         const double rr = lbx::prod0(r, r);
         double dr, ddum;
         if (stp == 1.0) { dr = gd - gdold; ddum = -gdold; }
         else { dr = (gd - gdold) * stp; d = d * stp; ddum = -gdold * stp; }
+        S.d = d;
         if (uni(dr <= kEpsMch * ddum)) {
-          updatd = false;
+          S.updatd = false;
         } else {
-          updatd = true;
-          rg.iupdat += 1;
-          if (rg.iupdat <= lbx::kM) {   // matupd
-            rg.col = rg.iupdat;
-            rg.itail = (rg.head + rg.iupdat - 1) % lbx::kM;
-          } else {
-            rg.itail = (rg.itail + 1) % lbx::kM;
-            rg.head = (rg.head + 1) % lbx::kM;
-          }
-          mem.ws(rg.itail) = d;
-          mem.wy(rg.itail) = r;
-          theta = rr / dr;
-          mem.ssd(rg.itail) = (stp == 1.0) ? dtd : stp * stp * dtd;
-          mem.syd(rg.itail) = dr;
-          if (uni(lbx::formt(mem, rg, theta) != 0)) restart();
+          S.updatd = true;
+          lbx::Ring rg = S.rg;
+          S.theta = rr / dr;
+          lbx::matupd(mem, rg, d, r, (stp == 1.0) ? S.dtd : stp * stp * S.dtd, dr);
+          S.rg = rg;
+          int ft;
+          NEMO_LBX_T(1, ft = lbx::formt(mem, rg, S.theta, L));
+          if (uni(ft != 0)) restart();
         }
       }
     }
     // ---- the next search direction (cauchy at col = 0; else formk + subsm)
     for (;;) {
-      if (uni(rg.col == 0)) {
+      double z;
+      const double theta = S.theta;
+      if (uni(S.rg.col == 0)) {
         const double neggi = -g;
         const double f1 = 0.0 - neggi * neggi;
         const double f2 = -theta * f1;
@@ -409,36 +504,59 @@ NEMO_LB LbfgsResult lbfgsb1_minimize_exact(FG& fg, double x0, lbx::Mem mem) {
         if (dtm <= 0.0) dtm = 0.0;
         z = fma_(0.0 + dtm, neggi, x);   // daxpy
       } else {
-        if (uni(updatd) && uni(lbx::formk(mem, rg, theta) != 0)) {
+        const lbx::Ring rg = S.rg;
+        int fk = 0;
+        if (uni(S.updatd)) NEMO_LBX_T(2, fk = lbx::formk(mem, rg, theta, L));
+        if (uni(fk != 0)) {
           restart();
           continue;
         }
         double zz = x;
-        if (uni(!lbx::subsm(mem, rg, theta, -g, x, zz))) {
+        bool ok;
+        NEMO_LBX_T(3, ok = lbx::subsm(mem, rg, theta, -g, x, zz, L));
+        if (uni(!ok)) {
           restart();
           continue;
         }
         z = zz;
       }
-      d = z - x;
-      dtd = lbx::prod0(d, d);
+      const double d = z - x;
+      S.z = z;
+      S.d = d;
+      S.dtd = lbx::prod0(d, d);
       const double dnorm = fabs(d);    // dnrm2, n = 1
-      stp = (nit == 0) ? dmin(1.0 / dnorm, kStpMax) : 1.0;
-      xk = x; fold = f; gold = g;
-      gdold = lbx::prod0(g, d);
+      const double stp = (S.nit == 0) ? dmin(1.0 / dnorm, kStpMax) : 1.0;
+      S.stp = stp;
+      S.xk = x; S.fold = f; S.gold = g;
+      const double gdold = lbx::prod0(g, d);
+      S.gdold = gdold;
       if (uni(gdold < 0.0)) {
-        ls.stpmax = kStpMax;
-        ls.start(stp, f, gdold);
-        ifun = 1;
-        in_ls = true;
-        x_eval = (stp == 1.0) ? z : stp * d + xk;
+        S.ls.stpmax = kStpMax;
+        S.ls.start(stp, f, gdold);
+        S.ifun = 1;
+        S.in_ls = true;
+        S.x_eval = (stp == 1.0) ? z : stp * d + x;
         break;
       }
       // lnsrlb: the directional derivative is not negative (info = -4)
-      if (uni(rg.col == 0)) return LbfgsResult{x, f, nit, nfev, 2};
+      if (uni(S.rg.col == 0)) return done(x, f, 2);
       restart();
     }
   }
+}
+
+// Minimise the reference's unbounded 1-D objective from x0 with scipy's
+// exact arithmetic (header); fg as lbfgsb1_minimize.  Status as there.
+template <class FG>
+NEMO_LB LbfgsResult lbfgsb1_minimize_exact(FG& fg, double x0, lbx::Mem mem) {
+  LbxState S;
+  lbx_init(S, x0);
+  while (lbx_run(S, mem)) {
+    double f0, f1;
+    fg(S.x_eval, S.x1, f0, f1);
+    lbx_feed(S, f0, f1);
+  }
+  return LbfgsResult{S.x, S.f, S.nit, S.nfev, S.status};
 }
 
 }  // namespace nemo

@@ -145,7 +145,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
-                  c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2};
+                  c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -199,6 +199,10 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_info, nc * S * S));
     HIPCHK(dalloc(&c.d_xcs, 2 * nc * E));
     HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
+    if (nemo::exact_supported(c)) {   // the exact local optima's c rows (nemo_exact.hip)
+      c.cap_xcbuf = (size_t)nc * nemo::pairs_per_chain(c.S, 0) * nemo::exact_cbuf_doubles(c);
+      HIPCHK(dalloc(&c.d_xcbuf, c.cap_xcbuf));
+    }
     c.cap_chains = nc;
   }
   return NEMO_OK;
@@ -343,6 +347,12 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     const int nb = c.cap_batch;
     c.cap_batch = 0;
     int rc2 = nemo_reserve(ctx, nb, 0);
+    if (rc2) return rc2;
+  }
+  if (c.cap_chains > 0 && nemo::exact_supported(c) && !c.d_xcbuf) {   // chains reserved before staging
+    const int nc = c.cap_chains;
+    c.cap_chains = 0;
+    int rc2 = nemo_reserve(ctx, 0, nc);
     if (rc2) return rc2;
   }
   c.staged = true;

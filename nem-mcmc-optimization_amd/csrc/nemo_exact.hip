@@ -33,23 +33,20 @@ using refmath::LdsTabs;
 
 // the SVML / glibc tables in LDS (per-lane indices)
 struct TabsLds {
-  double log_hi[16], log_lo[16], exp_hi[16], exp_lo[16];
+  alignas(16) double lrow[128][4];
+  alignas(16) double erow[16][2];
   uint64_t gexp[256];
-  uint32_t rbase[64], rin[64];
+  uint32_t rthr[64];
   __device__ void fill(int t, int nt) {
-    for (int q = t; q < 64; q += nt) {
-      rbase[q] = refmath::kRcp14Base[q];
-      rin[q] = refmath::kRcp14InBucket[q];
-    }
+    for (int q = t; q < 128; q += nt) refmath::svml_log_row((int)refmath::kRcp14Base[q >> 1] + (q & 1), lrow[q]);
+    for (int q = t; q < 64; q += nt) rthr[q] = refmath::kRcp14InBucket[q];
     for (int q = t; q < 16; q += nt) {
-      log_hi[q] = refmath::as_double(refmath::kSvmlLogHi[q]);
-      log_lo[q] = refmath::as_double(refmath::kSvmlLogLo[q]);
-      exp_hi[q] = refmath::as_double(refmath::kSvmlExpHi[q]);
-      exp_lo[q] = refmath::as_double(refmath::kSvmlExpLo[q]);
+      erow[q][0] = refmath::as_double(refmath::kSvmlExpHi[q]);
+      erow[q][1] = refmath::as_double(refmath::kSvmlExpLo[q]);
     }
     for (int q = t; q < 256; q += nt) gexp[q] = refmath::kGlibcExpTab[q];
   }
-  __device__ LdsTabs view() const { return LdsTabs{log_hi, log_lo, exp_hi, exp_lo, gexp, rbase, rin}; }
+  __device__ LdsTabs view() const { return LdsTabs{rthr, &lrow[0][0], &erow[0][0], gexp}; }
 };
 
 __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nwords, int j, int e) {
@@ -115,25 +112,57 @@ __global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch
   if (g >= (size_t)batch * E) return;
   const int b = (int)(g / E), e = (int)(g % E);
   double* col = cells + (size_t)b * (S + 1) * E + e;
+  // the rows are loaded two ahead of the (latency-bound) fold
   double acc = col[0];
-  for (int r = 1; r <= S; ++r) acc = refmath::logaddexp(acc, col[(size_t)r * E], tb);
+  double n1 = S >= 1 ? col[(size_t)E] : 0.0;
+  double n2 = S >= 2 ? col[(size_t)2 * E] : 0.0;
+  for (int r = 1; r <= S; ++r) {
+    const double cur = n1;
+    n1 = n2;
+    if (r + 2 <= S) n2 = col[(size_t)(r + 2) * E];
+    acc = refmath::logaddexp(acc, cur, tb);
+  }
   cs[(size_t)b * E + e] = acc;
   if (OW)
     for (int r = 0; r <= S; ++r) col[(size_t)r * E] = refmath::svml_exp(col[(size_t)r * E] - acc, tb);
 }
 
-// ll = sum(cs): Python's built-in sum, a left fold over the effects (one lane
-// per evaluation)
-__device__ __forceinline__ void seq_sum(const double* __restrict__ cs, int E, double* __restrict__ ll) {
-#pragma clang fp contract(off)
-  double acc = 0.0;
-  for (int e = 0; e < E; ++e) acc = acc + cs[e];
-  *ll = acc;
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__global__ void exact_seq_sum_kernel(int E, int batch, const double* __restrict__ cs, double* __restrict__ ll) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < batch) seq_sum(cs + (size_t)b * E, E, ll + b);
+// ll = sum(cs): Python's built-in sum, a left fold over the effects, by one
+// wave: 64 values per coalesced load (the next one in flight), then added in
+// order lane by lane from scalar registers; every lane holds the sum
+__device__ __forceinline__ double wave_seq_sum(const double* __restrict__ cs, int E, int lane) {
+#pragma clang fp contract(off)
+  double acc = 0.0;
+  double nxt = lane < E ? cs[lane] : 0.0;
+  for (int base = 0; base < E; base += kWave) {
+    const double v = nxt;
+    if (base + kWave < E) nxt = base + kWave + lane < E ? cs[base + kWave + lane] : 0.0;
+    const int n = E - base < kWave ? E - base : kWave;
+    if (n == kWave) {
+#pragma unroll
+      for (int l = 0; l < kWave; ++l) acc = acc + readlane_f64(v, l);
+    } else {
+      for (int l = 0; l < n; ++l) acc = acc + readlane_f64(v, l);
+    }
+  }
+  return acc;
+}
+
+// one wave per evaluation
+__global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, const double* __restrict__ cs,
+                                                            double* __restrict__ ll) {
+  const int b = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
+  const int lane = threadIdx.x & (kWave - 1);
+  if (b >= batch) return;
+  const double v = wave_seq_sum(cs + (size_t)b * E, E, lane);
+  if (lane == 0) ll[b] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -142,11 +171,17 @@ __global__ void exact_seq_sum_kernel(int E, int batch, const double* __restrict_
 // c * ex and + 1.0 rounded separately, SVML log, and numpy's pairwise sum
 // over the wave as laid out by host::build_pairwise_plan.
 // ---------------------------------------------------------------------------
-template <int NS>
+// c is read from memory at every evaluation (an L2 / MALL-resident copy), so
+// no register holds it while the optimiser runs: kPlan, the plan-ordered copy
+// the fused kernel writes ([NS][17][64]: chain element m of slot u at row u *
+// 17 + m, the remainder at row 16, one coalesced row per element); else the
+// caller's [E] vector at the plan's indices.
+template <int NS, bool kPlan>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
-  double c[NS][kChain];
-  double crem[NS];
+  static constexpr int kRows = kChain + 1;
+  const double* cp;
+  int cb[NS], rb[NS];   // kPlan: row offsets; else the chain's start / remainder index
   int cnt[NS], nrem[NS];
   bool hasrem[NS];
   int partner[8];
@@ -154,52 +189,94 @@ struct ExactObjective {
   double anc;
   LdsTabs tb;
 
-  __device__ __forceinline__ double sum_logs(double ex) const {
+  __device__ __forceinline__ double cval(int u, int m) const {
+    if (kPlan) return cp[cb[u] + m * kWave];
+    return m < cnt[u] ? cp[cb[u] + 8 * m] : 0.0;
+  }
+  __device__ __forceinline__ double crem(int u) const {
+    if (kPlan) return cp[rb[u]];
+    return hasrem[u] ? cp[rb[u]] : 0.0;
+  }
+
+  // both points of the forward difference in one pass over c (each point's
+  // own order of operations; two logs per element, grouped so that few are
+  // in flight at once)
+  __device__ __forceinline__ void sum_logs2(double ex0, double ex1, double& s0, double& s1) const {
 #pragma clang fp contract(off)
-    double res[NS];
+    // c is memory the compiler must read here, not values it carries over
+    // from the writes (that would hold them in registers through the optimiser)
+    __asm__ volatile("" ::: "memory");
+    double res0[NS], res1[NS];
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-      double acc = cnt[u] > 0 ? refmath::svml_log(c[u][0] * ex + 1.0, tb) : 0.0;
+      if (u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
+      double c[kChain];
 #pragma unroll
-      for (int m = 1; m < kChain; ++m) {
-        const double tm = refmath::svml_log(c[u][m] * ex + 1.0, tb);
-        acc = m < cnt[u] ? acc + tm : acc;
+      for (int m = 0; m < kChain; ++m) c[m] = cval(u, m);
+      const double cr = crem(u);
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int m = 0; m < kChain; ++m) {
+        const double t0 = refmath::svml_log(c[m] * ex0 + 1.0, tb);
+        const double t1 = refmath::svml_log(c[m] * ex1 + 1.0, tb);
+        if (m == 0) {
+          a0 = cnt[u] > 0 ? t0 : 0.0;
+          a1 = cnt[u] > 0 ? t1 : 0.0;
+        } else {
+          a0 = m < cnt[u] ? a0 + t0 : a0;
+          a1 = m < cnt[u] ? a1 + t1 : a1;
+        }
+        if (m & 1) __builtin_amdgcn_sched_barrier(0);
       }
       // the block's 8 accumulators: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
-      acc = acc + __shfl_xor(acc, 1);
-      acc = acc + __shfl_xor(acc, 2);
-      acc = acc + __shfl_xor(acc, 4);
+      a0 = a0 + __shfl_xor(a0, 1);
+      a1 = a1 + __shfl_xor(a1, 1);
+      a0 = a0 + __shfl_xor(a0, 2);
+      a1 = a1 + __shfl_xor(a1, 2);
+      a0 = a0 + __shfl_xor(a0, 4);
+      a1 = a1 + __shfl_xor(a1, 4);
       if (lb::uni(maxrem > 0)) {  // the block's n % 8 trailing elements, in order
-        const double tr = hasrem[u] ? refmath::svml_log(crem[u] * ex + 1.0, tb) : 0.0;
+        const double tr0 = hasrem[u] ? refmath::svml_log(cr * ex0 + 1.0, tb) : 0.0;
+        const double tr1 = hasrem[u] ? refmath::svml_log(cr * ex1 + 1.0, tb) : 0.0;
         for (int r = 0; r < 7; ++r) {
-          const double y = __shfl(tr, (lane & ~7) + r);
-          acc = r < nrem[u] ? acc + y : acc;
+          const double y0 = __shfl(tr0, (lane & ~7) + r);
+          const double y1 = __shfl(tr1, (lane & ~7) + r);
+          a0 = r < nrem[u] ? a0 + y0 : a0;
+          a1 = r < nrem[u] ? a1 + y1 : a1;
         }
       }
-      res[u] = acc;
+      res0[u] = a0;
+      res1[u] = a1;
     }
     // leaf L (slot L / 8, lanes 8 (L % 8) ..) to lane L
-    double v = 0.0;
+    double v0 = 0.0, v1 = 0.0;
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-      const double x = __shfl(res[u], 8 * (lane & 7));
-      v = (lane >> 3) == u ? x : v;
+      const double x0 = __shfl(res0[u], 8 * (lane & 7));
+      const double x1 = __shfl(res1[u], 8 * (lane & 7));
+      v0 = (lane >> 3) == u ? x0 : v0;
+      v1 = (lane >> 3) == u ? x1 : v1;
     }
     // the recursion's additions, one height at a time
-    for (int h = 0; h < nh; ++h) {
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      if (!lb::uni(h < nh)) break;
       const int p = partner[h];
-      const double y = __shfl(v, p < 0 ? lane : p);
-      v = p >= 0 ? v + y : v;
+      const double y0 = __shfl(v0, p < 0 ? lane : p);
+      const double y1 = __shfl(v1, p < 0 ? lane : p);
+      v0 = p >= 0 ? v0 + y0 : v0;
+      v1 = p >= 0 ? v1 + y1 : v1;
     }
-    return __shfl(v, 0);  // the root: its first leaf is leaf 0
+    s0 = __shfl(v0, 0);  // the root: its first leaf is leaf 0
+    s1 = __shfl(v1, 0);
   }
 
   __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
 #pragma clang fp contract(off)
     const double e0 = refmath::expit(x0, tb);
     const double e1 = refmath::expit(x1, tb);
-    const double p0 = sum_logs(e0);
-    const double p1 = sum_logs(e1);
+    double p0, p1;
+    sum_logs2(e0, e1, p0, p1);
     f0 = (-p0 + fabs(e0 - anc)) + e0 * (1.0 - e0);
     f1 = (-p1 + fabs(e1 - anc)) + e1 * (1.0 - e1);
   }
@@ -212,6 +289,7 @@ struct SeqSumArgs {
 };
 
 constexpr int kExactWaves = 4;
+constexpr int kStateDoubles = (int)((sizeof(LbxState) + 7) / 8);
 
 // one wave per (chain, permissible pair), kExactWaves per block; then the
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
@@ -221,15 +299,21 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
     int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
-    int32_t* __restrict__ info, int lo_blocks, SeqSumArgs fin) {
+    int32_t* __restrict__ info, double* __restrict__ cbuf, int lo_blocks, SeqSumArgs fin) {
 #pragma clang fp contract(off)
-  if ((int)blockIdx.x >= lo_blocks) {
-    const int bb = ((int)blockIdx.x - lo_blocks) * (int)blockDim.x + (int)threadIdx.x;
-    if (bb < fin.batch) seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, fin.ll + bb);
+  if ((int)blockIdx.x >= lo_blocks) {   // one wave per chain
+    const int bb = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - lo_blocks) * kExactWaves +
+                                                  (int)threadIdx.x / kWave);
+    const int ln = threadIdx.x & (kWave - 1);
+    if (bb < fin.batch) {
+      const double v = wave_seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, ln);
+      if (ln == 0) fin.ll[bb] = v;
+    }
     return;
   }
   __shared__ TabsLds tabs;
   __shared__ double mem[kExactWaves][lbx::kMemDoubles];
+  __shared__ double lst_raw[kExactWaves][kStateDoubles];   // LbxState (not trivially constructible)
   tabs.fill(threadIdx.x, blockDim.x);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
@@ -245,13 +329,15 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
   const double s = w01[idx];
   const double lvlo = xlo[k], lvhi = xhi[k];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
-  ExactObjective<NS> obj;
+  using Obj = ExactObjective<NS, true>;
+  Obj obj;
   obj.tb = tabs.view();
   obj.lane = lane;
   obj.nh = nh;
   obj.maxrem = maxrem;
   obj.anc = anc[idx];
-  // c = a / b, nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k]))
+  // c = a / b, nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k])), once,
+  // into this wave's plan-ordered rows
   auto cval = [&](int e) {
 #pragma clang fp contract(off)
     const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
@@ -259,20 +345,32 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
     const double bd = (1.0 - s * a) + s * (lv - 1.0);
     return a / bd;
   };
+  double* rows = cbuf + (size_t)gw * NS * Obj::kRows * kWave;
+  obj.cp = rows;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     const int q = u * kWave + lane;
-    const int st = plan[q], ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
+    const int ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
     obj.cnt[u] = ct;
     obj.nrem[u] = plan[3 * NS * kWave + q];
-#pragma unroll
-    for (int m = 0; m < ExactObjective<NS>::kChain; ++m) obj.c[u][m] = m < ct ? cval(st + 8 * m) : 0.0;
     obj.hasrem[u] = re >= 0;
-    obj.crem[u] = re >= 0 ? cval(re) : 0.0;
+    obj.cb[u] = u * Obj::kRows * kWave + lane;
+    obj.rb[u] = obj.cb[u] + Obj::kChain * kWave;
+#pragma unroll 4
+    for (int m = 0; m < Obj::kChain; ++m) rows[obj.cb[u] + m * kWave] = m < ct ? cval(plan[q] + 8 * m) : 0.0;
+    rows[obj.rb[u]] = re >= 0 ? cval(re) : 0.0;
   }
 #pragma unroll
   for (int h = 0; h < 8; ++h) obj.partner[h] = h < nh ? plan[4 * NS * kWave + h * kWave + lane] : -1;
-  const LbfgsResult r = lbfgsb1_minimize_exact(obj, s, lbx::Mem{mem[wv]});
+  __threadfence_block();   // the rows are read back by the same lanes
+  LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
+  lbx_init(st, s);
+  while (lbx_run(st, lbx::Mem{mem[wv]})) {
+    double f0, f1;
+    obj(st.x_eval, st.x1, f0, f1);
+    lbx_feed(st, f0, f1);
+  }
+  const LbfgsResult r{st.x, st.f, st.nit, st.nfev, st.status};
   if (lane == 0) {
     const double wx = refmath::expit(r.x, obj.tb);
     wnew[idx] = wx;
@@ -295,33 +393,40 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_generic_k
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ double mem[kExactWaves][lbx::kMemDoubles];
+  __shared__ double lst_raw[kExactWaves][kStateDoubles];   // LbxState (not trivially constructible)
   tabs.fill(threadIdx.x, blockDim.x);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
   const int p = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (p >= n) return;
-  const double* cp = cvec + (size_t)p * E;
-  ExactObjective<NS> obj;
+  ExactObjective<NS, false> obj;
   obj.tb = tabs.view();
   obj.lane = lane;
   obj.nh = nh;
   obj.maxrem = maxrem;
   obj.anc = anc[p];
+  obj.cp = cvec + (size_t)p * E;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     const int q = u * kWave + lane;
-    const int st = plan[q], ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
+    const int ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
     obj.cnt[u] = ct;
     obj.nrem[u] = plan[3 * NS * kWave + q];
-#pragma unroll
-    for (int m = 0; m < ExactObjective<NS>::kChain; ++m) obj.c[u][m] = m < ct ? cp[st + 8 * m] : 0.0;
     obj.hasrem[u] = re >= 0;
-    obj.crem[u] = re >= 0 ? cp[re] : 0.0;
+    obj.cb[u] = ct > 0 ? plan[q] : 0;
+    obj.rb[u] = re >= 0 ? re : 0;
   }
 #pragma unroll
   for (int h = 0; h < 8; ++h) obj.partner[h] = h < nh ? plan[4 * NS * kWave + h * kWave + lane] : -1;
-  const LbfgsResult r = lbfgsb1_minimize_exact(obj, x0[p], lbx::Mem{mem[wv]});
+  LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
+  lbx_init(st, x0[p]);
+  while (lbx_run(st, lbx::Mem{mem[wv]})) {
+    double f0, f1;
+    obj(st.x_eval, st.x1, f0, f1);
+    lbx_feed(st, f0, f1);
+  }
+  const LbfgsResult r{st.x, st.f, st.nit, st.nfev, st.status};
   if (lane == 0) {
     const int nit = r.nit < 4095 ? r.nit : 4095;
     const int nfev = r.nfev < 32767 ? r.nfev : 32767;
@@ -386,6 +491,8 @@ hipError_t launch_refmath_probe(int fn, int n, const double* d_x, const double* 
 
 bool exact_supported(const Ctx& c) { return c.factored && c.exact_ok && c.d_xlo && c.d_pwplan; }
 
+size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true>::kRows * kWave); }
+
 hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
   const int S = c.S, E = c.E;
@@ -400,7 +507,7 @@ hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const doub
   else exact_fold_kernel<false><<<fb, 256, 0, st>>>(S, E, batch, d_cells, d_cs);
   err = hipGetLastError();
   if (err != hipSuccess || !d_ll) return err;
-  exact_seq_sum_kernel<<<(batch + 63) / 64, 64, 0, st>>>(E, batch, d_cs, d_ll);
+  exact_seq_sum_kernel<<<(batch + 3) / 4, 256, 0, st>>>(E, batch, d_cs, d_ll);
   return hipGetLastError();
 }
 
@@ -409,16 +516,17 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
                                   double* d_wdag, int32_t* d_info, const double* d_cs1, double* d_ll1,
                                   hipStream_t st) {
   const int nw = nchains * npairs;
+  if ((size_t)nw * exact_cbuf_doubles(c) > c.cap_xcbuf) return hipErrorInvalidValue;
   const int lo_blocks = (nw + kExactWaves - 1) / kExactWaves;
   SeqSumArgs fin{d_cs1, c.E, nchains, d_ll1};
-  const int fin_blocks = d_ll1 ? (nchains + kExactWaves * kWave - 1) / (kExactWaves * kWave) : 0;
+  const int fin_blocks = d_ll1 ? (nchains + kExactWaves - 1) / kExactWaves : 0;
   const dim3 grid(lo_blocks + fin_blocks);
   switch (c.pw_ns) {
 #define NEMO_EXACT_NS(NSV)                                                                                         \
   case NSV:                                                                                                        \
     local_opt_exact_kernel<NSV><<<grid, kExactWaves * kWave, 0, st>>>(                                            \
         c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
-        c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, lo_blocks, fin);                                 \
+        c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                      \
     break;
     NEMO_EXACT_NS(1)
     NEMO_EXACT_NS(2)

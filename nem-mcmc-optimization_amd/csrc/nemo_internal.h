@@ -121,6 +121,8 @@ struct Ctx {
   int pw_ns = 0, pw_nh = 0, pw_maxrem = 0;
   double* d_xcs = nullptr;         // [2][chains][E] cs of the step's two evaluations
   double* d_xcells2 = nullptr;     // [chains][S+1][E] eval #2's cells
+  double* d_xcbuf = nullptr;       // [chains * pairs][exact_cbuf_doubles] the local optima's c, plan order
+  size_t cap_xcbuf = 0;            // its size in doubles
 
   // worst-case |ll error| of the fixed-point kernels (nemo_host.h):
   // fx_colsum[k] = sum_e min(colbits_e, k) over the staged D1 bits; auto takes
@@ -229,6 +231,7 @@ hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const doub
 
 // the reference's arithmetic (nemo_exact.hip): supported for this staging?
 bool exact_supported(const Ctx& c);
+size_t exact_cbuf_doubles(const Ctx& c);   // per local optimum
 // eval in the reference's order: cells into d_cells [batch][S+1][E] (with
 // want_ow: replaced by the order weights), cs into d_cs [batch][E], ll into
 // d_ll (nullable: left to the caller)

@@ -11,8 +11,8 @@
 // (refmath_tables.h, read from the installed libraries by
 // tools/gen_refmath_tables.py), the same fused multiply-adds and roundings
 // -- so a device evaluation gives the reference's bits.  tests/host/
-// refmath_check.cpp compares every function with the library itself over 10^8
-// inputs per range on the CPU, and tests/test_gpu_refmath.py the device builds
+// refmath_check.cpp compares every function with the library itself over 2 x
+// 10^7 inputs per range on the CPU, and tests/test_gpu_exact.py the device builds
 // with numpy / scipy on the GPU box.
 //
 // Domain: finite inputs in the ranges the path produces (documented per
@@ -46,47 +46,58 @@ namespace refmath {
 
 NEMO_RM double as_double(uint64_t u) { return __builtin_bit_cast(double, u); }
 
+NEMO_RM uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
+NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// svml_log's reduction row for n = the number of vrcp14 switch points at or
+// below the mantissa (kRcp14Switch): r = RNE_1/32(vrcp14pd(m)) = (32 - n) / 32,
+// the exponent adjustment (1 when r < 0.75) and T(r) = log_hi + log_lo
+NEMO_RM void svml_log_row(int n, double* row) {
+  const double r = (double)(32 - n) * 0.03125;
+  const int j = (int)(as_u64(r) >> 48) & 15;
+  row[0] = r;
+  row[1] = r < 0.75 ? 1.0 : 0.0;
+  row[2] = as_double(kSvmlLogHi[j]);
+  row[3] = as_double(kSvmlLogLo[j]);
+}
+
 // Where the functions read their tables: by default the constant arrays of
 // refmath_tables.h; a device kernel passes copies in LDS (per-lane indices)
 struct ConstTabs {
-  NEMO_RMM double log_hi(int j) const;
-  NEMO_RMM double log_lo(int j) const;
-  NEMO_RMM double exp_hi(int j) const;
-  NEMO_RMM double exp_lo(int j) const;
-  NEMO_RMM uint64_t gexp(int i) const;
-  NEMO_RMM int rcp_n(uint32_t p22) const;
-};
-struct LdsTabs {
-  const double* log_hi_p;   // [16]
-  const double* log_lo_p;   // [16]
-  const double* exp_hi_p;   // [16]
-  const double* exp_lo_p;   // [16]
-  const uint64_t* gexp_p;   // [256]
-  const uint32_t* rbase_p;  // [64] kRcp14Base
-  const uint32_t* rin_p;    // [64] kRcp14InBucket
-  NEMO_RMM double log_hi(int j) const { return log_hi_p[j]; }
-  NEMO_RMM double log_lo(int j) const { return log_lo_p[j]; }
-  NEMO_RMM double exp_hi(int j) const { return exp_hi_p[j]; }
-  NEMO_RMM double exp_lo(int j) const { return exp_lo_p[j]; }
-  NEMO_RMM uint64_t gexp(int i) const { return gexp_p[i]; }
-  // the bucketed form of the step function (equal for every prefix: tests)
-  NEMO_RMM int rcp_n(uint32_t p22) const {
-    const uint32_t b = p22 >> 16;
-    return (int)rbase_p[b] + (p22 >= rin_p[b] ? 1 : 0);
+  // svml_log: the row of the 22-bit mantissa prefix p22
+  NEMO_RMM void log_row(uint32_t p22, double& r, double& kadj, double& hi, double& lo) const {
+    int n = 0;
+    for (int t = 0; t < 16; ++t) n += p22 >= kRcp14Switch[t] ? 1 : 0;
+    double row[4];
+    svml_log_row(n, row);
+    r = row[0], kadj = row[1], hi = row[2], lo = row[3];
   }
+  NEMO_RMM void exp_row(int j, double& hi, double& lo) const {
+    hi = as_double(kSvmlExpHi[j]);
+    lo = as_double(kSvmlExpLo[j]);
+  }
+  NEMO_RMM uint64_t gexp(int i) const { return kGlibcExpTab[i]; }
 };
-NEMO_RM uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
-NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
-NEMO_RMM double ConstTabs::log_hi(int j) const { return as_double(kSvmlLogHi[j]); }
-NEMO_RMM double ConstTabs::log_lo(int j) const { return as_double(kSvmlLogLo[j]); }
-NEMO_RMM double ConstTabs::exp_hi(int j) const { return as_double(kSvmlExpHi[j]); }
-NEMO_RMM double ConstTabs::exp_lo(int j) const { return as_double(kSvmlExpLo[j]); }
-NEMO_RMM uint64_t ConstTabs::gexp(int i) const { return kGlibcExpTab[i]; }
-NEMO_RMM int ConstTabs::rcp_n(uint32_t p22) const {
-  int n = 0;
-  for (int t = 0; t < 16; ++t) n += p22 >= kRcp14Switch[t] ? 1 : 0;
-  return n;
-}
+// The LDS form: the step function bucketed by the top 6 bits of p22 (one
+// switch point at most per bucket, kRcp14InBucket) and svml_log's rows per
+// (bucket, above its switch point): two dependent reads per log.  Equal to
+// ConstTabs for every prefix (tests/test_exact_spec.py).
+struct LdsTabs {
+  const uint32_t* rthr_p;   // [64] kRcp14InBucket
+  const double* lrow_p;     // [64][2][4] svml_log_row(kRcp14Base[b] + above)
+  const double* erow_p;     // [16][2] SVML exp's 2^(j/16) hi, lo
+  const uint64_t* gexp_p;   // [256] glibc exp's table
+  NEMO_RMM void log_row(uint32_t p22, double& r, double& kadj, double& hi, double& lo) const {
+    const uint32_t b = p22 >> 16;
+    const double* row = lrow_p + 4 * (2 * b + (p22 >= rthr_p[b] ? 1 : 0));
+    r = row[0], kadj = row[1], hi = row[2], lo = row[3];
+  }
+  NEMO_RMM void exp_row(int j, double& hi, double& lo) const {
+    hi = erow_p[2 * j];
+    lo = erow_p[2 * j + 1];
+  }
+  NEMO_RMM uint64_t gexp(int i) const { return gexp_p[i]; }
+};
 
 // ---------------------------------------------------------------------------
 // glibc 2.35 exp (sysdeps/ieee754/dbl-64/e_exp.c, Szabolcs Nagy's table
@@ -266,13 +277,11 @@ NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   constexpr double kLn2Hi = 0x1.62e42fefa0000p-1, kLn2Lo = 0x1.cf79abc9e0000p-40;
   const uint64_t b = as_u64(x);
   const double m = as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-  double k = (double)((int)((b >> 52) & 0x7ff) - 1023);
   const uint32_t p22 = (uint32_t)(b >> 30) & 0x3fffff;
-  const int n = tb.rcp_n(p22);
-  const double r = (double)(32 - n) * 0.03125;
+  double r, kadj, thi, tlo;
+  tb.log_row(p22, r, kadj, thi, tlo);
+  const double k = (double)((int)((b >> 52) & 0x7ff) - 1023) + kadj;   // + 1 when r < 0.75
   const double R = fma_(r, m, -1.0);
-  if (r < 0.75) k = k + 1.0;
-  const int j = (int)(as_u64(r) >> 48) & 15;
   double p7 = fma_(R, C200, C240);
   double p1 = fma_(R, C180, C1c0);
   const double R2 = R * R;
@@ -281,13 +290,13 @@ NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   p1 = fma_(R2, p1, p7);
   const double R4 = R2 * R2;
   p9 = fma_(R2, p9, p8);
-  const double H = fma_(k, kLn2Hi, tb.log_hi(j));
+  const double H = fma_(k, kLn2Hi, thi);
   const double P = fma_(R4, p1, p9);
   const double S = H + R;
   const double D = S - H;
   const double E = R - D;
   const double Q = fma_(R2, P, E);
-  const double L = fma_(kLn2Lo, k, tb.log_lo(j));
+  const double L = fma_(kLn2Lo, k, tlo);
   return S + (Q + L);
 }
 
@@ -333,8 +342,9 @@ NEMO_RM double svml_exp(double x, const TB& tb = TB{}) {
   const double p11 = fma_(r, C340, C380);
   p12 = fma_(r2, p12, p9);
   p12 = fma_(r2, p12, p11);
-  const double thi = tb.exp_hi(j);
-  const double q = fma_(p12, r, tb.exp_lo(j));
+  double thi, tlo;
+  tb.exp_row(j, thi, tlo);
+  const double q = fma_(p12, r, tlo);
   const double y = fma_(thi, q, thi);
   const double kfl = __builtin_floor(kf);
   return __builtin_ldexp(y, (int)kfl);

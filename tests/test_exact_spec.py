@@ -129,6 +129,23 @@ def test_local_optima_equal_scipy_records_bit_for_bit(spec, name):
     assert np.array_equal(xs, z["xstar"]) and np.array_equal(fs, z["fun"])
 
 
+def test_long_local_optima_equal_scipy_bit_for_bit(spec):
+    """The C3 optima that run longest (nit 6..11: the memory of m = 10 pairs
+    full and its oldest pair dropped; tests/golden/make_localopt_long.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from make_localopt_long import long_cases
+    c, anc, x0, rec = long_cases()
+    c = np.ascontiguousarray(c)
+    n, e = c.shape
+    xs, fs = np.zeros(n), np.zeros(n)
+    nit, nfev, st = (np.zeros(n, np.int32) for _ in range(3))
+    spec.spec_local_opt(n, e, _p(c), _p(np.ascontiguousarray(anc)), _p(np.ascontiguousarray(x0)), _p(xs), _p(fs),
+                        nit.ctypes.data_as(_ip), nfev.ctypes.data_as(_ip), st.ctypes.data_as(_ip))
+    assert rec["nit"].max() == 11
+    assert np.array_equal(nit, rec["nit"]) and np.array_equal(nfev, rec["nfev"])
+    assert np.array_equal(xs, rec["xstar"]) and np.array_equal(fs, rec["fun"])
+
+
 @pytest.mark.parametrize("name,s,e,k", [("C2", 16, 500, 8), ("C3", 64, 2000, 3)])
 def test_order_scores_equal_reference_goldens_bit_for_bit(spec, name, s, e, k):
     """compute_cell_ratios + calculate_ll in the reference's order: ll, cs and

@@ -66,6 +66,22 @@ def test_exact_local_optima_equal_scipy_records(name):
     eng.close()
 
 
+def test_exact_long_local_optima_equal_scipy():
+    """The longest C3 optima (nit up to 11: the m = 10 memory full and its
+    oldest pair dropped; tests/golden/make_localopt_long.py)."""
+    import os
+    import sys
+    from conftest import REPO
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from make_localopt_long import long_cases
+    c, anc, x0, rec = long_cases()
+    eng = Engine(np.zeros((3, c.shape[1])), np.zeros((2, 2, c.shape[1])))
+    xs, fs, nit, nfev, st = eng.local_opt(c, anc, x0)
+    assert np.array_equal(nit, rec["nit"]) and np.array_equal(nfev, rec["nfev"])
+    assert _bits_equal(xs, rec["xstar"]) and _bits_equal(fs, rec["fun"])
+    eng.close()
+
+
 @pytest.mark.parametrize("name,s,e", [("C2", 16, 500), ("C3", 64, 2000)])
 def test_exact_scores_equal_reference_goldens(name, s, e):
     """calculate_ll of the golden orders and weights (<= 64 orders: a

@@ -9,5 +9,7 @@ TAILN=30 step tests 900 python -u -m pytest tests/test_gpu_exact.py tests/test_g
 [ -n "$NO_AB" ] && exit 0
 TAILN=8 step ab1 300 env AB_OPT=exact python tools/step_probe.py 1 || exit 1
 TAILN=8 step ab16 300 env AB_OPT=exact python tools/step_probe.py 16 || exit 1
-TAILN=2 step trace1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$P/trace1" -o t -- python "$R/tools/step_probe.py" 1 || exit 1
-cut -c1-140 "$P/trace1/t_kernel_stats.csv" | head -14
+for n in ${TRACE:-1 16}; do
+  TAILN=2 step trace$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$P/trace$n" -o t -- python "$R/tools/step_probe.py" $n || exit 1
+  cut -c1-140 "$P/trace$n/t_kernel_stats.csv" | head -8
+done
