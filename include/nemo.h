@@ -249,7 +249,12 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                0 = the fast kernels (scores within ~1e-9)
  *   "exact_ok"   (get only) 1 if the staging supports "exact" (factored
  *                tables, no parent cap, numpy's pairwise sum of E fits the
- *                wave plan) */
+ *                wave plan)
+ *   "exact_form" the exact local-optimum kernel's form (same bits): 0 auto
+ *                (default: latency form while chains x pairs <=
+ *                "exact_lat_waves", 4096 by default, throughput form beyond),
+ *                1 latency (two waves per SIMD, a slot's c loaded at once),
+ *                2 throughput (four waves per SIMD) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

@@ -102,6 +102,15 @@ NEMO_LB void lanes_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// lane l's value, to every lane
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#endif
 
 // One output of OpenBLAS dgemv_t_SKYLAKEX with alpha = -1 (A m x n
 // column-major, lda, m < 2048): y - A(:, c)' x for column c, in the order of
@@ -165,6 +174,7 @@ NEMO_LB double ob_gemv_t_m1_col(int m, int n, int c, const double* a, int lda, c
 
 // OpenBLAS dpotrf('U') for n <= 16 (potf2_U); returns info (0 or j + 1).
 // Row j's update (dgemv_t) and scaling by 1 / ajj: one column per lane.
+#if !defined(__HIP_DEVICE_COMPILE__)
 NEMO_LB int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 #pragma clang fp contract(off)
   for (int j = 0; j < n; ++j) {
@@ -190,6 +200,42 @@ NEMO_LB int ob_potrf_u(int n, double* a, int lda, Lanes L) {
   }
   return 0;
 }
+#else
+// On the wave lane c owns column c (n <= 16): it also accumulates ddot(c,
+// A(:, c), A(:, c)) -- for n < 16 a chain in row order -- as the rows of its
+// column become final, so step j starts from its diagonal at once.
+__device__ __forceinline__ int ob_potrf_u(int n, double* a, int lda, Lanes L) {
+#pragma clang fp contract(off)
+  const int ln = L.id;
+  double* mine = a + (long)(ln < n ? ln : 0) * lda;
+  double sd = 0.0;
+  for (int j = 0; j < n; ++j) {
+    double* cj = a + (long)j * lda;
+    double ajj = ln == j ? cj[j] - sd : 0.0;
+    ajj = readlane_d(ajj, j);
+    if (uni(ajj <= 0.0)) {   // potf2: a NaN goes on to the square root
+      if (ln == j) cj[j] = ajj;
+      lanes_sync();
+      return j + 1;
+    }
+    ajj = __builtin_sqrt(ajj);
+    if (ln == j) cj[j] = ajj;
+    const int i = n - j - 1;
+    if (i > 0) {
+      const double inv = 1.0 / ajj;
+      if (ln > j && ln < n) {
+        double v = mine[j];
+        if (j > 0) v = ob_gemv_t_m1_col(j, i, ln - j - 1, a + (long)(j + 1) * lda, lda, cj, v);
+        v = v * inv;
+        mine[j] = v;
+        sd = fma_(v, v, sd);
+      }
+    }
+    lanes_sync();
+  }
+  return 0;
+}
+#endif
 
 // dtrtrs('U', 'T', 'N') with one right-hand side (trsv_TUN); 0 or the index
 // + 1 of a zero diagonal (checked first, as dtrtrs does)
@@ -348,15 +394,15 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
 
 // subsm from z = x with r = -g (cmprlb, unconstrained): the Newton step;
 // false when a triangular solve is singular (the caller restarts)
-NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z, Lanes L) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z, Lanes) {
 #pragma clang fp contract(off)
   const int col = rg.col, c2 = 2 * col;
-  double* wv = mem.wv();   // (a local array would live in per-lane scratch on the device)
-  for (int i = L.id; i < col; i += L.n) {
+  double* wv = mem.wv();
+  for (int i = 0; i < col; ++i) {
     wv[i] = sum0(mem.wy(i), r);
     wv[col + i] = theta * sum0(mem.ws(i), r);
   }
-  lanes_sync();
   const double* wn = mem.wn();
   if (ob_trsv_tun(c2, wn, kLdN, wv) != 0) return false;
   for (int i = 0; i < col; ++i) wv[i] = -wv[i];
@@ -367,6 +413,61 @@ NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, d
   z = x + d;   // the projection step of L-BFGS-B 3.0 (no bounds: alpha = 1, same bits)
   return true;
 }
+#else
+// The same on the wave, the work vector in registers (lane i holds wv[i]):
+// the two triangular solves as pipelines over the lanes -- trsv_TUN's dot of
+// row i accumulated on lane i as each earlier entry becomes final (the chain
+// of ddot's order; rows >= 16 take ddot's 16-term block sum at step 16), and
+// trsv_NUN's axpy updates applied by each lane to its own entry -- so a step
+// costs one operation, not a dot product.
+__device__ __forceinline__ bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z,
+                                      Lanes L) {
+#pragma clang fp contract(off)
+  const int col = rg.col, c2 = 2 * col;
+  const int ln = L.id;
+  const double* wn = mem.wn();
+  for (int i = 0; i < c2; ++i)   // dtrtrs checks the diagonal first (both solves: the same diagonal)
+    if (uni(wn[i + (long)i * kLdN] == 0.0)) return false;
+  double b = 0.0;
+  if (ln < col) b = sum0(mem.wy(ln), r);
+  else if (ln < c2) b = theta * sum0(mem.ws(ln - col), r);
+  // trsv_TUN: b_i = (b_i - ddot(i, U(:, i), b)) / u_ii
+  const double* ucol = wn + (long)(ln < c2 ? ln : 0) * kLdN;   // this lane's column of U
+  double dot = 0.0;
+  for (int k = 0; k < c2; ++k) {
+    if (k == 16 && ln >= 16 && ln < c2) {   // ddot_k, n >= 16: 4 x 4 lanes over the first 16
+      double t[4];
+      for (int l = 0; l < 4; ++l) {
+        const double a0 = fma_(ucol[l], readlane_d(b, l), 0.0);
+        const double a1 = fma_(ucol[4 + l], readlane_d(b, 4 + l), 0.0);
+        const double a2 = fma_(ucol[8 + l], readlane_d(b, 8 + l), 0.0);
+        const double a3 = fma_(ucol[12 + l], readlane_d(b, 12 + l), 0.0);
+        t[l] = ((a0 + a1) + a2) + a3;
+      }
+      dot = (t[0] + t[2]) + (t[1] + t[3]);
+    }
+    if (ln == k) {
+      if (k > 0) b = b - dot;
+      b = b / ucol[k];
+    }
+    const double bk = readlane_d(b, k);
+    if (ln > k && ln < c2 && (ln < 16 || k >= 16)) dot = fma_(bk, ucol[k], dot);
+  }
+  if (ln < col) b = -b;
+  // trsv_NUN: b_j /= u_jj, then b_k -= b_j u_kj for k < j
+  for (int j = c2 - 1; j >= 0; --j) {
+    if (ln == j) b = b / wn[j + (long)j * kLdN];
+    const double nb = -readlane_d(b, j);
+    if (ln < j) b = fma_(nb, wn[ln + (long)j * kLdN], b);
+  }
+  double d = r;
+  for (int jy = 0; jy < col; ++jy)
+    d = d + mem.wy(jy) * readlane_d(b, jy) / theta + mem.ws(jy) * readlane_d(b, col + jy);
+  d = d * (1.0 / theta);
+  z = x + d;   // the projection step of L-BFGS-B 3.0 (no bounds: alpha = 1, same bits)
+  return true;
+}
+#endif
 
 }  // namespace lbx
 

@@ -1163,6 +1163,16 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.exact = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "exact_form") == 0) {
+    if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput)", value);
+    ctx->c.exact_form = value;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "exact_lat_waves") == 0) {
+    if (value < 0) return fail(NEMO_ERR_ARG, "exact_lat_waves %d", value);
+    ctx->c.exact_lat_waves = value;
+    return NEMO_OK;
+  }
   if (strcmp(name, "graphs") == 0) {
     ctx->c.graphs = value ? 1 : 0;
     return NEMO_OK;
@@ -1219,6 +1229,8 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "graphs") == 0) *value = c.graphs;
   else if (strcmp(name, "exact") == 0) *value = c.exact;
+  else if (strcmp(name, "exact_form") == 0) *value = c.exact_form;
+  else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;
   else if (strcmp(name, "step_host_sum") == 0) *value = c.step_host_sum;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;

@@ -97,11 +97,13 @@ __global__ __launch_bounds__(256) void exact_cells_kernel(int S, int E, int etil
 
 // ---------------------------------------------------------------------------
 // fold: one thread per (evaluation, effect): cs = logaddexp.reduce over the
-// S + 1 rows in order (numpy's reduction of axis 0), then, with OW, the order
-// weights exp(cell - cs) in place of the cells.
+// S + 1 rows in order (numpy's reduction of axis 0).  The chain of S
+// logaddexps is the step's serial latency at one chain, so the rows come in
+// register blocks of 16, the next block's loads in flight during the fold of
+// the current one.  The order weights exp(cell - cs) follow in a separate,
+// fully parallel launch.
 // ---------------------------------------------------------------------------
-template <bool OW>
-__global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch, double* __restrict__ cells,
+__global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch, const double* __restrict__ cells,
                                                          double* __restrict__ cs) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
@@ -111,46 +113,71 @@ __global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch
   const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (g >= (size_t)batch * E) return;
   const int b = (int)(g / E), e = (int)(g % E);
-  double* col = cells + (size_t)b * (S + 1) * E + e;
-  // the rows are loaded two ahead of the (latency-bound) fold
-  double acc = col[0];
-  double n1 = S >= 1 ? col[(size_t)E] : 0.0;
-  double n2 = S >= 2 ? col[(size_t)2 * E] : 0.0;
-  for (int r = 1; r <= S; ++r) {
-    const double cur = n1;
-    n1 = n2;
-    if (r + 2 <= S) n2 = col[(size_t)(r + 2) * E];
-    acc = refmath::logaddexp(acc, cur, tb);
+  const double* col = cells + (size_t)b * (S + 1) * E + e;
+  const int R = S + 1;
+  constexpr int kC = 16;
+  double nxt[kC];
+#pragma unroll
+  for (int q = 0; q < kC; ++q) nxt[q] = q < R ? col[(size_t)q * E] : 0.0;
+  double acc = 0.0;
+  for (int r0 = 0; r0 < R; r0 += kC) {
+    double cur[kC];
+#pragma unroll
+    for (int q = 0; q < kC; ++q) cur[q] = nxt[q];
+    if (r0 + kC < R) {
+#pragma unroll
+      for (int q = 0; q < kC; ++q) nxt[q] = r0 + kC + q < R ? col[(size_t)(r0 + kC + q) * E] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kC; ++q) {
+      const int r = r0 + q;
+      if (r < R) acc = r == 0 ? cur[q] : refmath::logaddexp(acc, cur[q], tb);
+    }
   }
   cs[(size_t)b * E + e] = acc;
-  if (OW)
-    for (int r = 0; r <= S; ++r) col[(size_t)r * E] = refmath::svml_exp(col[(size_t)r * E] - acc, tb);
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+// order weights in place: cell = exp(cell - cs) (nem_order_mcmc.py:92), one
+// thread per cell
+__global__ __launch_bounds__(256) void exact_ow_kernel(int S, int E, int batch, double* __restrict__ cells,
+                                                       const double* __restrict__ cs) {
+#pragma clang fp contract(off)
+  __shared__ TabsLds tabs;
+  tabs.fill(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t n = (size_t)batch * (S + 1) * E;
+  if (g >= n) return;
+  const int e = (int)(g % E);
+  const size_t b = g / ((size_t)(S + 1) * E);
+  cells[g] = refmath::svml_exp(cells[g] - cs[b * E + e], tabs.view());
 }
 
 // ll = sum(cs): Python's built-in sum, a left fold over the effects, by one
-// wave: 64 values per coalesced load (the next one in flight), then added in
-// order lane by lane from scalar registers; every lane holds the sum
-__device__ __forceinline__ double wave_seq_sum(const double* __restrict__ cs, int E, int lane) {
+// wave: 64 values per coalesced load (the next one in flight), staged in the
+// wave's LDS row and added in order from broadcast reads, which issue ahead
+// of the chain of additions; every lane holds the sum
+__device__ __forceinline__ double wave_seq_sum(const double* __restrict__ cs, int E, int lane, double* row) {
 #pragma clang fp contract(off)
   double acc = 0.0;
   double nxt = lane < E ? cs[lane] : 0.0;
   for (int base = 0; base < E; base += kWave) {
     const double v = nxt;
     if (base + kWave < E) nxt = base + kWave + lane < E ? cs[base + kWave + lane] : 0.0;
+    row[lane] = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int n = E - base < kWave ? E - base : kWave;
     if (n == kWave) {
 #pragma unroll
-      for (int l = 0; l < kWave; ++l) acc = acc + readlane_f64(v, l);
+      for (int l = 0; l < kWave; ++l) acc = acc + row[l];
     } else {
-      for (int l = 0; l < n; ++l) acc = acc + readlane_f64(v, l);
+      for (int l = 0; l < n; ++l) acc = acc + row[l];
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   return acc;
 }
@@ -158,10 +185,11 @@ __device__ __forceinline__ double wave_seq_sum(const double* __restrict__ cs, in
 // one wave per evaluation
 __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, const double* __restrict__ cs,
                                                             double* __restrict__ ll) {
+  __shared__ double rows[4][kWave];
   const int b = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (b >= batch) return;
-  const double v = wave_seq_sum(cs + (size_t)b * E, E, lane);
+  const double v = wave_seq_sum(cs + (size_t)b * E, E, lane, rows[threadIdx.x / kWave]);
   if (lane == 0) ll[b] = v;
 }
 
@@ -175,32 +203,38 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // no register holds it while the optimiser runs: kPlan, the plan-ordered copy
 // the fused kernel writes ([NS][17][64]: chain element m of slot u at row u *
 // 17 + m, the remainder at row 16, one coalesced row per element); else the
-// caller's [E] vector at the plan's indices.
-template <int NS, bool kPlan>
+// caller's [E] vector at the plan's indices.  The plan itself (per lane:
+// chain starts, counts, remainders, tree partners) is the block's LDS copy.
+template <int NS, bool kPlan, bool kLat>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
   const double* cp;
-  int cb[NS], rb[NS];   // kPlan: row offsets; else the chain's start / remainder index
-  int cnt[NS], nrem[NS];
-  bool hasrem[NS];
-  int partner[8];
+  const int32_t* pl;   // host::PairwisePlan rows in LDS: start, cnt, rem, nrem [NS][64], partner [8][64]
   int nh, maxrem, lane;
   double anc;
   LdsTabs tb;
 
-  __device__ __forceinline__ double cval(int u, int m) const {
-    if (kPlan) return cp[cb[u] + m * kWave];
-    return m < cnt[u] ? cp[cb[u] + 8 * m] : 0.0;
+  __device__ __forceinline__ int start(int u) const { return pl[u * kWave + lane]; }
+  __device__ __forceinline__ int cnt(int u) const { return pl[(NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int rem(int u) const { return pl[(2 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int nrem(int u) const { return pl[(3 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int partner(int h) const { return pl[(4 * NS + h) * kWave + lane]; }
+
+  __device__ __forceinline__ double cval(int u, int m, int cu) const {
+    if (kPlan) return cp[(u * kRows + m) * kWave + lane];
+    return m < cu ? cp[start(u) + 8 * m] : 0.0;
   }
-  __device__ __forceinline__ double crem(int u) const {
-    if (kPlan) return cp[rb[u]];
-    return hasrem[u] ? cp[rb[u]] : 0.0;
+  __device__ __forceinline__ double crem(int u, int ru) const {
+    if (kPlan) return cp[(u * kRows + kChain) * kWave + lane];
+    return ru >= 0 ? cp[ru] : 0.0;
   }
 
   // both points of the forward difference in one pass over c (each point's
-  // own order of operations; two logs per element, grouped so that few are
-  // in flight at once)
+  // own order of operations).  kLat (few optima per SIMD: the step's time is
+  // one optimum's latency): a slot's 16 c values loaded at once, the logs in
+  // pairs of elements; else (many per SIMD: throughput) the chain loop
+  // unrolled by 4 with c read as it goes -- fewer registers, more waves.
   __device__ __forceinline__ void sum_logs2(double ex0, double ex1, double& s0, double& s1) const {
 #pragma clang fp contract(off)
     // c is memory the compiler must read here, not values it carries over
@@ -209,24 +243,32 @@ struct ExactObjective {
     double res0[NS], res1[NS];
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-      if (u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
-      double c[kChain];
-#pragma unroll
-      for (int m = 0; m < kChain; ++m) c[m] = cval(u, m);
-      const double cr = crem(u);
+      const int cu = cnt(u);
       double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-      for (int m = 0; m < kChain; ++m) {
-        const double t0 = refmath::svml_log(c[m] * ex0 + 1.0, tb);
-        const double t1 = refmath::svml_log(c[m] * ex1 + 1.0, tb);
+      auto step = [&](int m, double cm) {
+        const double t0 = refmath::svml_log(cm * ex0 + 1.0, tb);
+        const double t1 = refmath::svml_log(cm * ex1 + 1.0, tb);
         if (m == 0) {
-          a0 = cnt[u] > 0 ? t0 : 0.0;
-          a1 = cnt[u] > 0 ? t1 : 0.0;
+          a0 = cu > 0 ? t0 : 0.0;
+          a1 = cu > 0 ? t1 : 0.0;
         } else {
-          a0 = m < cnt[u] ? a0 + t0 : a0;
-          a1 = m < cnt[u] ? a1 + t1 : a1;
+          a0 = m < cu ? a0 + t0 : a0;
+          a1 = m < cu ? a1 + t1 : a1;
         }
-        if (m & 1) __builtin_amdgcn_sched_barrier(0);
+      };
+      if (kLat) {
+        if (u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
+        double c[kChain];
+#pragma unroll
+        for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
+#pragma unroll
+        for (int m = 0; m < kChain; ++m) {
+          step(m, c[m]);
+          if (m & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll 4
+        for (int m = 0; m < kChain; ++m) step(m, cval(u, m, cu));
       }
       // the block's 8 accumulators: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
       a0 = a0 + __shfl_xor(a0, 1);
@@ -236,13 +278,15 @@ struct ExactObjective {
       a0 = a0 + __shfl_xor(a0, 4);
       a1 = a1 + __shfl_xor(a1, 4);
       if (lb::uni(maxrem > 0)) {  // the block's n % 8 trailing elements, in order
-        const double tr0 = hasrem[u] ? refmath::svml_log(cr * ex0 + 1.0, tb) : 0.0;
-        const double tr1 = hasrem[u] ? refmath::svml_log(cr * ex1 + 1.0, tb) : 0.0;
+        const int ru = rem(u), nr = nrem(u);
+        const double cr = crem(u, ru);
+        const double tr0 = ru >= 0 ? refmath::svml_log(cr * ex0 + 1.0, tb) : 0.0;
+        const double tr1 = ru >= 0 ? refmath::svml_log(cr * ex1 + 1.0, tb) : 0.0;
         for (int r = 0; r < 7; ++r) {
           const double y0 = __shfl(tr0, (lane & ~7) + r);
           const double y1 = __shfl(tr1, (lane & ~7) + r);
-          a0 = r < nrem[u] ? a0 + y0 : a0;
-          a1 = r < nrem[u] ? a1 + y1 : a1;
+          a0 = r < nr ? a0 + y0 : a0;
+          a1 = r < nr ? a1 + y1 : a1;
         }
       }
       res0[u] = a0;
@@ -261,7 +305,7 @@ struct ExactObjective {
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
       if (!lb::uni(h < nh)) break;
-      const int p = partner[h];
+      const int p = partner(h);
       const double y0 = __shfl(v0, p < 0 ? lane : p);
       const double y1 = __shfl(v1, p < 0 ? lane : p);
       v0 = p >= 0 ? v0 + y0 : v0;
@@ -282,6 +326,13 @@ struct ExactObjective {
   }
 };
 
+// the plan's rows to LDS (every thread of the block)
+template <int NS>
+__device__ __forceinline__ void plan_to_lds(const int32_t* __restrict__ plan, int nh, int32_t* lds) {
+  const int n = (4 * NS + nh) * kWave;
+  for (int q = threadIdx.x; q < (4 * NS + 8) * kWave; q += blockDim.x) lds[q] = q < n ? plan[q] : -1;
+}
+
 struct SeqSumArgs {
   const double* cs = nullptr;
   int E = 0, batch = 0;
@@ -293,28 +344,31 @@ constexpr int kStateDoubles = (int)((sizeof(LbxState) + 7) / 8);
 
 // one wave per (chain, permissible pair), kExactWaves per block; then the
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
-template <int NS>
-__global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
+template <int NS, bool kLat>
+__global__ __launch_bounds__(kExactWaves * kWave)
+__attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_exact_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
     int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
     int32_t* __restrict__ info, double* __restrict__ cbuf, int lo_blocks, SeqSumArgs fin) {
 #pragma clang fp contract(off)
+  __shared__ TabsLds tabs;
+  __shared__ double mem[kExactWaves][lbx::kMemDoubles];
+  __shared__ double lst_raw[kExactWaves][kStateDoubles];   // LbxState (not trivially constructible)
+  __shared__ int32_t pl[(4 * NS + 8) * kWave];
   if ((int)blockIdx.x >= lo_blocks) {   // one wave per chain
     const int bb = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - lo_blocks) * kExactWaves +
                                                   (int)threadIdx.x / kWave);
     const int ln = threadIdx.x & (kWave - 1);
     if (bb < fin.batch) {
-      const double v = wave_seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, ln);
+      const double v = wave_seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, ln, &mem[threadIdx.x / kWave][0]);
       if (ln == 0) fin.ll[bb] = v;
     }
     return;
   }
-  __shared__ TabsLds tabs;
-  __shared__ double mem[kExactWaves][lbx::kMemDoubles];
-  __shared__ double lst_raw[kExactWaves][kStateDoubles];   // LbxState (not trivially constructible)
   tabs.fill(threadIdx.x, blockDim.x);
+  plan_to_lds<NS>(plan, nh, pl);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
@@ -329,9 +383,10 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
   const double s = w01[idx];
   const double lvlo = xlo[k], lvhi = xhi[k];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
-  using Obj = ExactObjective<NS, true>;
+  using Obj = ExactObjective<NS, true, kLat>;
   Obj obj;
   obj.tb = tabs.view();
+  obj.pl = pl;
   obj.lane = lane;
   obj.nh = nh;
   obj.maxrem = maxrem;
@@ -349,19 +404,12 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
   obj.cp = rows;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
-    const int q = u * kWave + lane;
-    const int ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
-    obj.cnt[u] = ct;
-    obj.nrem[u] = plan[3 * NS * kWave + q];
-    obj.hasrem[u] = re >= 0;
-    obj.cb[u] = u * Obj::kRows * kWave + lane;
-    obj.rb[u] = obj.cb[u] + Obj::kChain * kWave;
+    const int st = obj.start(u), ct = obj.cnt(u), re = obj.rem(u);
+    double* row = rows + u * Obj::kRows * kWave + lane;
 #pragma unroll 4
-    for (int m = 0; m < Obj::kChain; ++m) rows[obj.cb[u] + m * kWave] = m < ct ? cval(plan[q] + 8 * m) : 0.0;
-    rows[obj.rb[u]] = re >= 0 ? cval(re) : 0.0;
+    for (int m = 0; m < Obj::kChain; ++m) row[m * kWave] = m < ct ? cval(st + 8 * m) : 0.0;
+    row[Obj::kChain * kWave] = re >= 0 ? cval(re) : 0.0;
   }
-#pragma unroll
-  for (int h = 0; h < 8; ++h) obj.partner[h] = h < nh ? plan[4 * NS * kWave + h * kWave + lane] : -1;
   __threadfence_block();   // the rows are read back by the same lanes
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
@@ -387,38 +435,30 @@ __global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_kernel(
 // calculate_local_optimum of one pair, and the scipy records of the tests);
 // out [n][3] = x*, f*, packed info
 template <int NS>
-__global__ __launch_bounds__(kExactWaves * kWave) void local_opt_exact_generic_kernel(
+__global__ __launch_bounds__(kExactWaves * kWave)
+__attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_generic_kernel(
     int E, int n, const double* __restrict__ cvec, const double* __restrict__ anc, const double* __restrict__ x0,
     const int32_t* __restrict__ plan, int nh, int maxrem, double* __restrict__ out) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ double mem[kExactWaves][lbx::kMemDoubles];
   __shared__ double lst_raw[kExactWaves][kStateDoubles];   // LbxState (not trivially constructible)
+  __shared__ int32_t pl[(4 * NS + 8) * kWave];
   tabs.fill(threadIdx.x, blockDim.x);
+  plan_to_lds<NS>(plan, nh, pl);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
   const int p = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (p >= n) return;
-  ExactObjective<NS, false> obj;
+  ExactObjective<NS, false, true> obj;
   obj.tb = tabs.view();
+  obj.pl = pl;
   obj.lane = lane;
   obj.nh = nh;
   obj.maxrem = maxrem;
   obj.anc = anc[p];
   obj.cp = cvec + (size_t)p * E;
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    const int q = u * kWave + lane;
-    const int ct = plan[NS * kWave + q], re = plan[2 * NS * kWave + q];
-    obj.cnt[u] = ct;
-    obj.nrem[u] = plan[3 * NS * kWave + q];
-    obj.hasrem[u] = re >= 0;
-    obj.cb[u] = ct > 0 ? plan[q] : 0;
-    obj.rb[u] = re >= 0 ? re : 0;
-  }
-#pragma unroll
-  for (int h = 0; h < 8; ++h) obj.partner[h] = h < nh ? plan[4 * NS * kWave + h * kWave + lane] : -1;
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, x0[p]);
   while (lbx_run(st, lbx::Mem{mem[wv]})) {
@@ -491,7 +531,7 @@ hipError_t launch_refmath_probe(int fn, int n, const double* d_x, const double* 
 
 bool exact_supported(const Ctx& c) { return c.factored && c.exact_ok && c.d_xlo && c.d_pwplan; }
 
-size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true>::kRows * kWave); }
+size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true, true>::kRows * kWave); }
 
 hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
@@ -503,9 +543,13 @@ hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const doub
   if (err != hipSuccess) return err;
   const size_t nthr = (size_t)batch * E;
   const int fb = (int)((nthr + 255) / 256);
-  if (want_ow) exact_fold_kernel<true><<<fb, 256, 0, st>>>(S, E, batch, d_cells, d_cs);
-  else exact_fold_kernel<false><<<fb, 256, 0, st>>>(S, E, batch, d_cells, d_cs);
+  exact_fold_kernel<<<fb, 256, 0, st>>>(S, E, batch, d_cells, d_cs);
   err = hipGetLastError();
+  if (err == hipSuccess && want_ow) {
+    const size_t ncell = (size_t)batch * (S + 1) * E;
+    exact_ow_kernel<<<(unsigned)((ncell + 255) / 256), 256, 0, st>>>(S, E, batch, d_cells, d_cs);
+    err = hipGetLastError();
+  }
   if (err != hipSuccess || !d_ll) return err;
   exact_seq_sum_kernel<<<(batch + 3) / 4, 256, 0, st>>>(E, batch, d_cs, d_ll);
   return hipGetLastError();
@@ -521,12 +565,20 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   SeqSumArgs fin{d_cs1, c.E, nchains, d_ll1};
   const int fin_blocks = d_ll1 ? (nchains + kExactWaves - 1) / kExactWaves : 0;
   const dim3 grid(lo_blocks + fin_blocks);
+  // the latency form while the optima fit in two waves per SIMD (the GPU's
+  // 256 CUs x 4 SIMDs); the throughput form (four per SIMD) beyond
+  const bool lat = c.exact_form == 1 || (c.exact_form == 0 && nw <= c.exact_lat_waves);
   switch (c.pw_ns) {
 #define NEMO_EXACT_NS(NSV)                                                                                         \
   case NSV:                                                                                                        \
-    local_opt_exact_kernel<NSV><<<grid, kExactWaves * kWave, 0, st>>>(                                            \
-        c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
-        c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                      \
+    if (lat)                                                                                                       \
+      local_opt_exact_kernel<NSV, true><<<grid, kExactWaves * kWave, 0, st>>>(                                    \
+          c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
+          c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                    \
+    else                                                                                                           \
+      local_opt_exact_kernel<NSV, false><<<grid, kExactWaves * kWave, 0, st>>>(                                   \
+          c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
+          c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                    \
     break;
     NEMO_EXACT_NS(1)
     NEMO_EXACT_NS(2)

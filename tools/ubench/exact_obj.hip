@@ -28,7 +28,9 @@ __global__ __launch_bounds__(kExactWaves * kWave) void obj_bench_kernel(int W, i
                                                                          const int32_t* __restrict__ plan, int nh,
                                                                          int maxrem, double* __restrict__ out) {
   __shared__ TabsLds tabs;
+  __shared__ int32_t pl[(4 * NS + 8) * kWave];
   tabs.fill(threadIdx.x, blockDim.x);
+  plan_to_lds<NS>(plan, nh, pl);
   __syncthreads();
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
@@ -36,22 +38,12 @@ __global__ __launch_bounds__(kExactWaves * kWave) void obj_bench_kernel(int W, i
   using Obj = ExactObjective<NS, true>;
   Obj obj;
   obj.tb = tabs.view();
+  obj.pl = pl;
   obj.lane = lane;
   obj.nh = nh;
   obj.maxrem = maxrem;
   obj.anc = 0.25;
   obj.cp = cbuf + (size_t)gw * NS * Obj::kRows * kWave;
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    const int q = u * kWave + lane;
-    obj.cnt[u] = plan[NS * kWave + q];
-    obj.nrem[u] = plan[3 * NS * kWave + q];
-    obj.hasrem[u] = plan[2 * NS * kWave + q] >= 0;
-    obj.cb[u] = u * Obj::kRows * kWave + lane;
-    obj.rb[u] = obj.cb[u] + Obj::kChain * kWave;
-  }
-#pragma unroll
-  for (int h = 0; h < 8; ++h) obj.partner[h] = h < nh ? plan[4 * NS * kWave + h * kWave + lane] : -1;
   double acc = 0.0;
   for (int k = 0; k < K; ++k) {
     const double x = 0.3 * k - 0.6;
