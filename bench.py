@@ -669,6 +669,14 @@ def main():
                 cb.run(n_it)
                 walls.append(time.perf_counter() - t0)
             e2e[tag] = (float(np.median(walls)), cb.best_scores, walls)
+        # the same sampler with the fast kernels (the host's share of a step)
+        eng.set_option("exact", 0)
+        ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pool).run(2)
+        cbf = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pool)
+        t0 = time.perf_counter()
+        cbf.run(n_it)
+        e2e_fast = time.perf_counter() - t0
+        eng.set_option("exact", 1)
         pool.close()
         dt = e2e["pool"][0]
         extras["mcmc_end_to_end"] = {
@@ -678,6 +686,8 @@ def main():
             "includes": f"ChainBatch.run: proposals, reset quirks, ancestor_x (scipy getrf/getri in {nw} "
                         "InvPool worker processes) and accept per chain on the host + the fused device step",
             "ms_per_step_serial_inv": 1e3 * e2e["serial"][0] / n_it,
+            "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
+            "ms_per_step_fast_kernels": 1e3 * e2e_fast / n_it,
             "pool_bits_equal_serial": bool(np.array_equal(e2e["pool"][1], e2e["serial"][1])),
             "reference_cpu_s_per_chain_step": 1.2}
         if args.config == "C3":

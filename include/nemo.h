@@ -239,7 +239,9 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                bits; measured slower for one chain, so 0 = auto never
  *                takes it), 1 = never, 3 = the same on a 2-wave block
  *   "exact"      1 (default): nemo_optimal_weights, nemo_local_opt and the
- *                ll-only nemo_score of <= 64 orders compute in the
+ *                ll-only host-pointer nemo_score (any batch; with
+ *                "fact_kernel" 0 -- an explicitly chosen kernel runs as
+ *                chosen -- and no effective cap) compute in the
  *                reference's own arithmetic -- numpy's SVML log / exp, glibc's
  *                exp / log1p, numpy's pairwise sum and scipy's compact-form
  *                L-BFGS-B with OpenBLAS's small kernels, restated bit for bit

@@ -512,10 +512,13 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
   const size_t S = c.S, E = c.E;
   hipStream_t st = c.stream;
-  if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.exact && cap == 0 && nemo::exact_supported(c) &&
-      batch <= 64) {
-    // ll only for a sampler (calculate_ll / compute_ll of a few orders): the
-    // reference's arithmetic (nemo_exact.hip), pos and W in one copy
+  if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.exact && c.fact_kernel == 0 &&
+      (cap == 0 || cap >= (int)S - 1) && nemo::exact_supported(c)) {
+    // ll only (a sampler's calculate_ll / compute_ll): the reference's
+    // arithmetic (nemo_exact.hip) whatever the batch, so a score never
+    // depends on how many orders share the call; pos and W in one copy.  An
+    // explicitly chosen kernel (option fact_kernel) runs as chosen; the
+    // batched device entry (nemo_score_dev) keeps the fixed-point kernels.
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t n = batch, o_w01 = up(n * S * 4), o_ll = o_w01 + up(n * S * S * 8), total = o_ll + up(n * 8);
     if ((rc = step_stage(c, 0, total))) return rc;

@@ -215,11 +215,31 @@ struct ExactObjective {
   double anc;
   LdsTabs tb;
 
+  // kLat: the plan's per-lane values also in registers (load_plan), off the
+  // evaluation's critical path; else read from LDS where used
+  int r_cnt[kLat ? NS : 1], r_rem[kLat ? NS : 1], r_nrem[kLat ? NS : 1], r_partner[kLat ? 8 : 1];
+
+  __device__ __forceinline__ void load_plan() {
+    if (kLat) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        r_cnt[u] = pl[(NS + u) * kWave + lane];
+        r_rem[u] = pl[(2 * NS + u) * kWave + lane];
+        r_nrem[u] = pl[(3 * NS + u) * kWave + lane];
+      }
+#pragma unroll
+      for (int h = 0; h < 8; ++h) r_partner[h] = pl[(4 * NS + h) * kWave + lane];
+    }
+  }
   __device__ __forceinline__ int start(int u) const { return pl[u * kWave + lane]; }
-  __device__ __forceinline__ int cnt(int u) const { return pl[(NS + u) * kWave + lane]; }
-  __device__ __forceinline__ int rem(int u) const { return pl[(2 * NS + u) * kWave + lane]; }
-  __device__ __forceinline__ int nrem(int u) const { return pl[(3 * NS + u) * kWave + lane]; }
-  __device__ __forceinline__ int partner(int h) const { return pl[(4 * NS + h) * kWave + lane]; }
+  __device__ __forceinline__ int cnt(int u) const { return kLat ? r_cnt[kLat ? u : 0] : pl[(NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int rem(int u) const { return kLat ? r_rem[kLat ? u : 0] : pl[(2 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int nrem(int u) const {
+    return kLat ? r_nrem[kLat ? u : 0] : pl[(3 * NS + u) * kWave + lane];
+  }
+  __device__ __forceinline__ int partner(int h) const {
+    return kLat ? r_partner[kLat ? h : 0] : pl[(4 * NS + h) * kWave + lane];
+  }
 
   __device__ __forceinline__ double cval(int u, int m, int cu) const {
     if (kPlan) return cp[(u * kRows + m) * kWave + lane];
@@ -391,6 +411,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   obj.nh = nh;
   obj.maxrem = maxrem;
   obj.anc = anc[idx];
+  obj.load_plan();
   // c = a / b, nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k])), once,
   // into this wave's plan-ordered rows
   auto cval = [&](int e) {
@@ -459,6 +480,7 @@ __attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_generic_kernel(
   obj.maxrem = maxrem;
   obj.anc = anc[p];
   obj.cp = cvec + (size_t)p * E;
+  obj.load_plan();
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, x0[p]);
   while (lbx_run(st, lbx::Mem{mem[wv]})) {

@@ -248,16 +248,74 @@ NEMO_RM double glibc_log1p(double x) {
   return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
 }
 
-// numpy's npy_logaddexp (npymath, float64): glibc exp and log1p
+// glibc_log1p for x in [0, 1] (logaddexp's argument exp(-|x - y|)) without
+// branches on the common paths: the k = 0 branch (x < 0.41422) and the
+// normalising branch (x >= 0.41422, one more division) computed together and
+// selected per lane -- in a wave whose lanes take both, the branchy form runs
+// both anyway.  The tiny and |f| < 2^-20 cases stay branches (rare).  Same
+// bits as glibc_log1p on [0, 1] (tests/host/refmath_check.cpp).
+NEMO_RM double log1p_unit(double x) {
+  NEMO_RM_NOCONTRACT
+  constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  constexpr double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+                   Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+                   Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+                   Lp7 = 1.479819860511658591e-01;
+  const int32_t hx = (int32_t)(as_u64(x) >> 32);
+  // x >= 0.41422: u = 1 + x normalised to [sqrt(2)/2, sqrt(2)), k its exponent
+  const double u = 1.0 + x;
+  const int32_t hu0 = (int32_t)(as_u64(u) >> 32);
+  int32_t kb = (hu0 >> 20) - 1023;
+  double cb = kb > 0 ? 1.0 - (u - x) : x - (u - 1.0);
+  cb = cb / u;
+  int32_t hum = hu0 & 0x000fffff;
+  const bool up = hum >= 0x6a09e;
+  const uint64_t lo = as_u64(u) & 0xffffffffull;
+  const double un = as_double(((uint64_t)(uint32_t)(hum | (up ? 0x3fe00000 : 0x3ff00000)) << 32) | lo);
+  kb = up ? kb + 1 : kb;
+  hum = up ? (0x00100000 - hum) >> 2 : hum;
+  const bool big = hx >= 0x3FDA827A;
+  const double f = big ? un - 1.0 : x;
+  const int32_t k = big ? kb : 0;
+  const double c = big ? cb : 0.0;
+  const int32_t hu = big ? hum : 1;
+  const double hfsq = 0.5 * f * f;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double R1 = z * Lp1, z2 = z * z;
+  const double R2 = Lp2 + z * Lp3, z4 = z2 * z2;
+  const double R3 = Lp4 + z * Lp5, z6 = z4 * z2;
+  const double R4 = Lp6 + z * Lp7;
+  const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+  double r = k == 0 ? f - (hfsq - s * (hfsq + R))
+                    : k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+  if (hu == 0) {  // |f| < 2^-20 (x = 1 here)
+    if (f == 0.0) {
+      r = k == 0 ? 0.0 : k * ln2_hi + (c + k * ln2_lo);
+    } else {
+      const double Rs = hfsq * (1.0 - 0.66666666666666666 * f);
+      r = k == 0 ? f - Rs : k * ln2_hi - ((Rs - (k * ln2_lo + c)) - f);
+    }
+  }
+  if (hx < 0x3e200000) r = hx < 0x3c900000 ? x : x - x * x * 0.5;  // |x| < 2^-29
+  return r;
+}
+
+// numpy's npy_logaddexp (npymath, float64): glibc exp and log1p; the two
+// branches on the sign of x - y select their operands instead (one exp and
+// one log1p per lane, not one of each per branch taken in the wave)
 template <class TB = ConstTabs>
 NEMO_RM double logaddexp(double x, double y, const TB& tb = TB{}) {
   NEMO_RM_NOCONTRACT
   constexpr double kLogE2 = 0.693147180559945309417232121458176568;
-  if (x == y) return x + kLogE2;
   const double tmp = x - y;
-  if (tmp > 0) return x + glibc_log1p(glibc_exp(-tmp, tb));
-  if (tmp <= 0) return y + glibc_log1p(glibc_exp(tmp, tb));
-  return tmp;
+  const bool pos = tmp > 0;
+  const double m = pos ? x : y;
+  const double a = pos ? -tmp : tmp;   // -|x - y|
+  double r = m + log1p_unit(glibc_exp(a, tb));
+  if (tmp != tmp) r = tmp;
+  if (x == y) r = x + kLogE2;
+  return r;
 }
 
 // ---------------------------------------------------------------------------

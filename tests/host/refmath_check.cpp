@@ -79,6 +79,30 @@ static double libm_exp(double x) { return exp(x); }
 static double libm_log1p(double x) { return log1p(x); }
 static double my_exp(double x) { return glibc_exp(x); }
 static double my_log1p(double x) { return glibc_log1p(x); }
+static double my_log1p_unit(double x) { return log1p_unit(x); }
+// npymath's npy_logaddexp over libm's exp / log1p
+static double npy_logaddexp(double x, double y) {
+  if (x == y) return x + 0.693147180559945309417232121458176568;
+  const double tmp = x - y;
+  if (tmp > 0) return x + log1p(exp(-tmp));
+  if (tmp <= 0) return y + log1p(exp(tmp));
+  return tmp;
+}
+static Stat check_lae(long n, double lo, double hi, double spread) {
+  Stat s;
+  for (long i = 0; i < n; ++i) {
+    const double x = uni(lo, hi);
+    double y = x + uni(-spread, spread);
+    if ((next_u64() & 15) == 0) y = x;
+    const double a = npy_logaddexp(x, y), b = logaddexp(x, y);
+    if (memcmp(&a, &b, 8) != 0) {
+      if (!s.bad) s.first = x;
+      s.bad++;
+    }
+    s.n++;
+  }
+  return s;
+}
 static double my_slog(double x) { return svml_log(x); }
 static double my_sexp(double x) { return svml_exp(x); }
 
@@ -105,6 +129,13 @@ int main(int argc, char** argv) {
            return (next_u64() & 1 ? 1 : -1) * loguni(1e-20, 1); }, n), fails);
   report("glibc log1p (0, 1] (logaddexp)", check_scalar(libm_log1p, my_log1p, [] { return loguni(1e-300, 1); }, n), fails);
   report("glibc log1p (-1, 100]", check_scalar(libm_log1p, my_log1p, [] { return uni(-0.999999, 100); }, n), fails);
+  report("log1p_unit (0, 1]", check_scalar(libm_log1p, my_log1p_unit, [] { return loguni(1e-300, 1); }, n), fails);
+  report("log1p_unit [0.4, 1]", check_scalar(libm_log1p, my_log1p_unit, [] { return uni(0.4, 1.0); }, n), fails);
+  report("log1p_unit sqrt(2) - 1 +- 1e-5", check_scalar(libm_log1p, my_log1p_unit, [] { return uni(0.41420, 0.41424); }, n), fails);
+  report("log1p_unit 1 - [0, 1e-15]", check_scalar(libm_log1p, my_log1p_unit, [] { return 1.0 - uni(0, 1e-15); }, n), fails);
+  report("logaddexp spread 5", check_lae(n, -3000, 0, 5), fails);
+  report("logaddexp spread 800", check_lae(n, -3000, 0, 800), fails);
+  report("logaddexp spread 1e-14", check_lae(n, -100, 100, 1e-14), fails);
   report("svml log  [1, 1e6] (1 + c e)", check_svml(slog, my_slog, [] { return loguni(1, 1e6); }, n), fails);
   report("svml log  [1e-3, 10]", check_svml(slog, my_slog, [] { return loguni(1e-3, 10); }, n), fails);
   report("svml log  1 + [1e-12, 1e-2]", check_svml(slog, my_slog, [] { return 1.0 + loguni(1e-12, 1e-2); }, n), fails);

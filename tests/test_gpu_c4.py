@@ -107,4 +107,11 @@ def test_bench_timed_region_gathers_over_rccl(rccl_world1, c3):
     wall, kern_ms, _ = bench.timed_steps(eng, torch, b, 0, 3, 1, d_pos, d_w01, d_ll, stream, 1, dist,
                                          collective=True)
     assert wall > 0 and kern_ms > 0
-    assert np.array_equal(d_ll.cpu().numpy(), eng.score(pos, w01))
+    # the timed region runs the batched fixed-point kernel: the host call with
+    # the fast kernels gives its bits (the exact arithmetic is within 1e-6)
+    eng.set_option("exact", 0)
+    try:
+        assert np.array_equal(d_ll.cpu().numpy(), eng.score(pos, w01))
+    finally:
+        eng.set_option("exact", 1)
+    assert np.max(np.abs(d_ll.cpu().numpy() - eng.score(pos, w01))) <= 1e-6

@@ -565,6 +565,7 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     pos = np.array([rng.permutation(s) for _ in range(b)], dtype=np.int32)
     w01 = expit(rng.uniform(-3, 3, (b, s, s)))
     eng.set_option("fact_kernel", 0)
+    eng.set_option("exact", 0)   # the fixed-point kernels (the exact path: test_gpu_exact.py)
     big = eng.score(pos, w01)
     for n in (1, 5, 64):
         assert np.array_equal(eng.score(pos[:n], w01[:n]), big[:n])
@@ -610,6 +611,11 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     eng.set_option("score_path", 1)
     assert np.max(np.abs(eng.score(pos[:8], w01[:8]) - big[:8])) <= 1e-8
     eng.set_option("score_path", 0)
+    eng.set_option("exact", 1)
+    # the exact arithmetic: batch-independent too, within 1e-6 of the kernels
+    ex = eng.score(pos, w01)
+    assert np.array_equal(eng.score(pos[:5], w01[:5]), ex[:5])
+    assert np.max(np.abs(ex - big)) <= 1e-6
 
 
 def test_replica_exchange_net2_golden(net2):
