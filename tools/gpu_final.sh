@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 P=${PROF_DIR:-gpurun_out/final}
 PROF_DIR=$P PMC=1 bash tools/gpu_round.sh || exit 1
-PROF_DIR=$P/c3 STALLS=1 bash tools/gpu_prof.sh || exit 1
-PROF_DIR=$P/w128 CONFIG=W128 bash tools/gpu_prof.sh || exit 1
-PROF_DIR=$P/c5 CONFIG=C5 bash tools/gpu_prof.sh || exit 1
-PROF_DIR=$P/stream NEMO_BENCH_BATCH=128 BENCH_ARGS="--path stream" bash tools/gpu_prof.sh || exit 1
+PROF_DIR=$P/c3 STALLS=1 bash tools/gpu_tasks.sh prof || exit 1
+PROF_DIR=$P/w128 CONFIG=W128 bash tools/gpu_tasks.sh prof || exit 1
+PROF_DIR=$P/c5 CONFIG=C5 bash tools/gpu_tasks.sh prof || exit 1
+PROF_DIR=$P/stream NEMO_BENCH_BATCH=128 BENCH_ARGS="--path stream" bash tools/gpu_tasks.sh prof || exit 1
