@@ -512,13 +512,15 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
   const size_t S = c.S, E = c.E;
   hipStream_t st = c.stream;
-  if (!cs_out && !cells_out && !ow_out && use_factored(c) && c.exact && c.fact_kernel == 0 &&
+  if (!(cells_out && ow_out) && use_factored(c) && c.exact && c.fact_kernel == 0 &&
       (cap == 0 || cap >= (int)S - 1) && nemo::exact_supported(c)) {
-    // ll only (a sampler's calculate_ll / compute_ll): the reference's
-    // arithmetic (nemo_exact.hip) whatever the batch, so a score never
-    // depends on how many orders share the call; pos and W in one copy.  An
-    // explicitly chosen kernel (option fact_kernel) runs as chosen; the
-    // batched device entry (nemo_score_dev) keeps the fixed-point kernels.
+    // the reference's arithmetic (nemo_exact.hip) whatever the batch, so a
+    // score never depends on how many orders share the call: ll and, when
+    // asked, the column sums cs and the order weights (calculate_ll's ow) or
+    // the cells (the order weights are written over the cells, so not both);
+    // pos and W in one copy.  An explicitly chosen kernel (option
+    // fact_kernel) runs as chosen; the batched device entry (nemo_score_dev)
+    // keeps the fixed-point kernels.
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t n = batch, o_w01 = up(n * S * 4), o_ll = o_w01 + up(n * S * S * 8), total = o_ll + up(n * 8);
     if ((rc = step_stage(c, 0, total))) return rc;
@@ -528,8 +530,11 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
     memcpy(hs + o_w01, w01, n * S * S * 8);
     HIPCHK(hipMemcpyAsync(ds, hs, o_ll, hipMemcpyHostToDevice, st));
     HIPCHK(nemo::launch_exact_eval(c, batch, (const int32_t*)ds, (const double*)(ds + o_w01), c.d_ow, c.d_cs,
-                                   (double*)(ds + o_ll), false, st));
+                                   (double*)(ds + o_ll), ow_out != nullptr, st));
     HIPCHK(hipMemcpyAsync(hs + o_ll, ds + o_ll, n * 8, hipMemcpyDeviceToHost, st));
+    if (cs_out) HIPCHK(hipMemcpyAsync(cs_out, c.d_cs, n * E * 8, hipMemcpyDeviceToHost, st));
+    if (ow_out || cells_out)
+      HIPCHK(hipMemcpyAsync(ow_out ? ow_out : cells_out, c.d_ow, n * (S + 1) * E * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     memcpy(ll_out, hs + o_ll, n * 8);
     c.ow_chains = 0;  // d_ow no longer holds fused-step order weights
@@ -1167,13 +1172,19 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "exact_form") == 0) {
-    if (value < 0 || value > 2) return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput)", value);
+    if (value < 0 || value > 3)
+      return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair)", value);
     ctx->c.exact_form = value;
     return NEMO_OK;
   }
   if (strcmp(name, "exact_lat_waves") == 0) {
     if (value < 0) return fail(NEMO_ERR_ARG, "exact_lat_waves %d", value);
     ctx->c.exact_lat_waves = value;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "exact_pair_waves") == 0) {
+    if (value < 0) return fail(NEMO_ERR_ARG, "exact_pair_waves %d", value);
+    ctx->c.exact_pair_waves = value;
     return NEMO_OK;
   }
   if (strcmp(name, "graphs") == 0) {
@@ -1234,6 +1245,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact") == 0) *value = c.exact;
   else if (strcmp(name, "exact_form") == 0) *value = c.exact_form;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
+  else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;
   else if (strcmp(name, "step_host_sum") == 0) *value = c.step_host_sum;
   else if (strcmp(name, "win") == 0) *value = c.win_ok ? 1 : 0;

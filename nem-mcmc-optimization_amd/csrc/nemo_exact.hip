@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // 17 + m, the remainder at row 16, one coalesced row per element); else the
 // caller's [E] vector at the plan's indices.  The plan itself (per lane:
 // chain starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat>
+template <int NS, bool kPlan, bool kLat, bool kPair = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
@@ -217,10 +217,11 @@ struct ExactObjective {
 
   // kLat: the plan's per-lane values also in registers (load_plan), off the
   // evaluation's critical path; else read from LDS where used
-  int r_cnt[kLat ? NS : 1], r_rem[kLat ? NS : 1], r_nrem[kLat ? NS : 1], r_partner[kLat ? 8 : 1];
+  static constexpr bool kRegs = kLat || kPair;
+  int r_cnt[kRegs ? NS : 1], r_rem[kRegs ? NS : 1], r_nrem[kRegs ? NS : 1], r_partner[kRegs ? 8 : 1];
 
   __device__ __forceinline__ void load_plan() {
-    if (kLat) {
+    if (kRegs) {
 #pragma unroll
       for (int u = 0; u < NS; ++u) {
         r_cnt[u] = pl[(NS + u) * kWave + lane];
@@ -232,13 +233,15 @@ struct ExactObjective {
     }
   }
   __device__ __forceinline__ int start(int u) const { return pl[u * kWave + lane]; }
-  __device__ __forceinline__ int cnt(int u) const { return kLat ? r_cnt[kLat ? u : 0] : pl[(NS + u) * kWave + lane]; }
-  __device__ __forceinline__ int rem(int u) const { return kLat ? r_rem[kLat ? u : 0] : pl[(2 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int cnt(int u) const { return kRegs ? r_cnt[kRegs ? u : 0] : pl[(NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int rem(int u) const {
+    return kRegs ? r_rem[kRegs ? u : 0] : pl[(2 * NS + u) * kWave + lane];
+  }
   __device__ __forceinline__ int nrem(int u) const {
-    return kLat ? r_nrem[kLat ? u : 0] : pl[(3 * NS + u) * kWave + lane];
+    return kRegs ? r_nrem[kRegs ? u : 0] : pl[(3 * NS + u) * kWave + lane];
   }
   __device__ __forceinline__ int partner(int h) const {
-    return kLat ? r_partner[kLat ? h : 0] : pl[(4 * NS + h) * kWave + lane];
+    return kRegs ? r_partner[kRegs ? h : 0] : pl[(4 * NS + h) * kWave + lane];
   }
 
   __device__ __forceinline__ double cval(int u, int m, int cu) const {
@@ -255,64 +258,63 @@ struct ExactObjective {
   // one optimum's latency): a slot's 16 c values loaded at once, the logs in
   // pairs of elements; else (many per SIMD: throughput) the chain loop
   // unrolled by 4 with c read as it goes -- fewer registers, more waves.
-  __device__ __forceinline__ void sum_logs2(double ex0, double ex1, double& s0, double& s1) const {
+  // one slot's chain sums of both points after the 8-accumulator combine and
+  // the block's tail elements (the leaf values of its 8 blocks, on lanes 8 L)
+  __device__ __forceinline__ void slot_sums(int u, double ex0, double ex1, double& a0, double& a1) const {
 #pragma clang fp contract(off)
-    // c is memory the compiler must read here, not values it carries over
-    // from the writes (that would hold them in registers through the optimiser)
-    __asm__ volatile("" ::: "memory");
-    double res0[NS], res1[NS];
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const int cu = cnt(u);
-      double a0 = 0.0, a1 = 0.0;
-      auto step = [&](int m, double cm) {
-        const double t0 = refmath::svml_log(cm * ex0 + 1.0, tb);
-        const double t1 = refmath::svml_log(cm * ex1 + 1.0, tb);
-        if (m == 0) {
-          a0 = cu > 0 ? t0 : 0.0;
-          a1 = cu > 0 ? t1 : 0.0;
-        } else {
-          a0 = m < cu ? a0 + t0 : a0;
-          a1 = m < cu ? a1 + t1 : a1;
-        }
-      };
-      if (kLat) {
-        if (u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
-        double c[kChain];
-#pragma unroll
-        for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
-#pragma unroll
-        for (int m = 0; m < kChain; ++m) {
-          step(m, c[m]);
-          if (m & 1) __builtin_amdgcn_sched_barrier(0);
-        }
+    const int cu = cnt(u);
+    a0 = 0.0;
+    a1 = 0.0;
+    auto step = [&](int m, double cm) {
+      const double t0 = refmath::svml_log(cm * ex0 + 1.0, tb);
+      const double t1 = refmath::svml_log(cm * ex1 + 1.0, tb);
+      if (m == 0) {
+        a0 = cu > 0 ? t0 : 0.0;
+        a1 = cu > 0 ? t1 : 0.0;
       } else {
+        a0 = m < cu ? a0 + t0 : a0;
+        a1 = m < cu ? a1 + t1 : a1;
+      }
+    };
+    if (kLat) {
+      double c[kChain];
+#pragma unroll
+      for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
+#pragma unroll
+      for (int m = 0; m < kChain; ++m) {
+        step(m, c[m]);
+        if (m & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
 #pragma unroll 4
-        for (int m = 0; m < kChain; ++m) step(m, cval(u, m, cu));
-      }
-      // the block's 8 accumulators: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
-      a0 = a0 + __shfl_xor(a0, 1);
-      a1 = a1 + __shfl_xor(a1, 1);
-      a0 = a0 + __shfl_xor(a0, 2);
-      a1 = a1 + __shfl_xor(a1, 2);
-      a0 = a0 + __shfl_xor(a0, 4);
-      a1 = a1 + __shfl_xor(a1, 4);
-      if (lb::uni(maxrem > 0)) {  // the block's n % 8 trailing elements, in order
-        const int ru = rem(u), nr = nrem(u);
-        const double cr = crem(u, ru);
-        const double tr0 = ru >= 0 ? refmath::svml_log(cr * ex0 + 1.0, tb) : 0.0;
-        const double tr1 = ru >= 0 ? refmath::svml_log(cr * ex1 + 1.0, tb) : 0.0;
-        for (int r = 0; r < 7; ++r) {
-          const double y0 = __shfl(tr0, (lane & ~7) + r);
-          const double y1 = __shfl(tr1, (lane & ~7) + r);
-          a0 = r < nr ? a0 + y0 : a0;
-          a1 = r < nr ? a1 + y1 : a1;
-        }
-      }
-      res0[u] = a0;
-      res1[u] = a1;
+      for (int m = 0; m < kChain; ++m) step(m, cval(u, m, cu));
     }
-    // leaf L (slot L / 8, lanes 8 (L % 8) ..) to lane L
+    // the block's 8 accumulators: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+    a0 = a0 + __shfl_xor(a0, 1);
+    a1 = a1 + __shfl_xor(a1, 1);
+    a0 = a0 + __shfl_xor(a0, 2);
+    a1 = a1 + __shfl_xor(a1, 2);
+    a0 = a0 + __shfl_xor(a0, 4);
+    a1 = a1 + __shfl_xor(a1, 4);
+    if (lb::uni(maxrem > 0)) {  // the block's n % 8 trailing elements, in order
+      const int ru = rem(u), nr = nrem(u);
+      const double cr = crem(u, ru);
+      const double tr0 = ru >= 0 ? refmath::svml_log(cr * ex0 + 1.0, tb) : 0.0;
+      const double tr1 = ru >= 0 ? refmath::svml_log(cr * ex1 + 1.0, tb) : 0.0;
+      for (int r = 0; r < 7; ++r) {
+        const double y0 = __shfl(tr0, (lane & ~7) + r);
+        const double y1 = __shfl(tr1, (lane & ~7) + r);
+        a0 = r < nr ? a0 + y0 : a0;
+        a1 = r < nr ? a1 + y1 : a1;
+      }
+    }
+  }
+
+  // the leaves to the root: leaf L (slot L / 8, lanes 8 (L % 8) ..) to lane
+  // L, then the recursion's additions one height at a time
+  __device__ __forceinline__ void tree(const double (&res0)[NS], const double (&res1)[NS], double& s0,
+                                       double& s1) const {
+#pragma clang fp contract(off)
     double v0 = 0.0, v1 = 0.0;
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
@@ -321,7 +323,6 @@ struct ExactObjective {
       v0 = (lane >> 3) == u ? x0 : v0;
       v1 = (lane >> 3) == u ? x1 : v1;
     }
-    // the recursion's additions, one height at a time
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
       if (!lb::uni(h < nh)) break;
@@ -335,7 +336,47 @@ struct ExactObjective {
     s1 = __shfl(v1, 0);
   }
 
-  __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) const {
+  // the pair form (kPair: two waves per optimum, the slots split between
+  // them, u % 2 == half): each wave's slot sums meet in LDS (double-buffered
+  // by evaluation parity), then both waves form the same root
+  double* xres = nullptr;   // [2][NS][64][2] in LDS
+  int half = 0, par = 0;
+
+  __device__ __forceinline__ void sum_logs2(double ex0, double ex1, double& s0, double& s1) {
+#pragma clang fp contract(off)
+    // c is memory the compiler must read here, not values it carries over
+    // from the writes (that would hold them in registers through the optimiser)
+    __asm__ volatile("" ::: "memory");
+    double res0[NS], res1[NS];
+    if (kPair) {
+      double* xr = xres + (size_t)par * NS * kWave * 2;
+      par ^= 1;
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        if ((u & 1) != half) continue;
+        if (u > 1) __asm__ volatile("" ::: "memory");
+        double a0, a1;
+        slot_sums(u, ex0, ex1, a0, a1);
+        xr[(u * kWave + lane) * 2] = a0;
+        xr[(u * kWave + lane) * 2 + 1] = a1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        res0[u] = xr[(u * kWave + lane) * 2];
+        res1[u] = xr[(u * kWave + lane) * 2 + 1];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        if (kLat && u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
+        slot_sums(u, ex0, ex1, res0[u], res1[u]);
+      }
+    }
+    tree(res0, res1, s0, s1);
+  }
+
+  __device__ __forceinline__ void operator()(double x0, double x1, double& f0, double& f1) {
 #pragma clang fp contract(off)
     const double e0 = refmath::expit(x0, tb);
     const double e1 = refmath::expit(x1, tb);
@@ -448,6 +489,99 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
       const int nit = r.nit < 4095 ? r.nit : 4095;
       const int nfev = r.nfev < 32767 ? r.nfev : 32767;
       info[idx] = (int32_t)(r.status | (nit << 4) | (nfev << 16));
+    }
+  }
+}
+
+// The pair form (few optima: a step's time is its slowest optimum): two waves
+// per (chain, pair), one block each, the objective's slots split between
+// them (u % 2 == the wave) and met in LDS per evaluation; both waves run the
+// same optimiser on their own copy of its state, so they take the same path
+// and the same number of barriers.  Appended blocks as above (two chains per
+// block).
+template <int NS>
+__global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4))) void local_opt_exact_pair_kernel(
+    int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
+    const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
+    const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
+    int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
+    int32_t* __restrict__ info, double* __restrict__ cbuf, int lo_blocks, SeqSumArgs fin) {
+#pragma clang fp contract(off)
+  __shared__ TabsLds tabs;
+  __shared__ double mem[2][lbx::kMemDoubles];
+  __shared__ double lst_raw[2][kStateDoubles];
+  __shared__ double xres[2 * NS * kWave * 2];
+  const int wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if ((int)blockIdx.x >= lo_blocks) {   // one wave per chain
+    const int bb = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - lo_blocks) * 2 + wv);
+    if (bb < fin.batch) {
+      const double v = wave_seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, lane, &mem[wv][0]);
+      if (lane == 0) fin.ll[bb] = v;
+    }
+    return;
+  }
+  tabs.fill(threadIdx.x, blockDim.x);
+  __syncthreads();
+  const int gw = blockIdx.x;   // the optimum: uniform over the block
+  if (gw >= nchains * npairs) return;
+  const int b = gw / npairs;
+  const int n = gw - b * npairs;
+  const int pk = pairs[(size_t)b * S * S + n];
+  const int i = pk >> 16;
+  const int k = pk & 0xffff;
+  const size_t idx = ((size_t)b * S + i) * S + k;
+  const double s = w01[idx];
+  const double lvlo = xlo[k], lvhi = xhi[k];
+  const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
+  // the throughput form's objective (few registers: four waves per SIMD
+  // hold the 2 x 2016 waves of one chain's step), its plan in registers
+  // (read once from global memory: no LDS copy, so eight blocks fit a CU)
+  using Obj = ExactObjective<NS, true, false, true>;
+  Obj obj;
+  obj.tb = tabs.view();
+  obj.pl = plan;
+  obj.lane = lane;
+  obj.nh = nh;
+  obj.maxrem = maxrem;
+  obj.anc = anc[idx];
+  obj.xres = xres;
+  obj.half = wv;
+  obj.load_plan();
+  auto cval = [&](int e) {
+#pragma clang fp contract(off)
+    const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
+    const double a = (lv - 1.0) * owk[e];
+    const double bd = (1.0 - s * a) + s * (lv - 1.0);
+    return a / bd;
+  };
+  double* rows = cbuf + (size_t)gw * NS * Obj::kRows * kWave;
+  obj.cp = rows;
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {   // this wave's slots' rows (it alone reads them)
+    if ((u & 1) != wv) continue;
+    const int st = obj.start(u), ct = obj.cnt(u), re = obj.rem(u);
+    double* row = rows + u * Obj::kRows * kWave + lane;
+#pragma unroll 4
+    for (int m = 0; m < Obj::kChain; ++m) row[m * kWave] = m < ct ? cval(st + 8 * m) : 0.0;
+    row[Obj::kChain * kWave] = re >= 0 ? cval(re) : 0.0;
+  }
+  __threadfence_block();
+  LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
+  lbx_init(st, s);
+  while (lbx_run(st, lbx::Mem{mem[wv]})) {
+    double f0, f1;
+    obj(st.x_eval, st.x1, f0, f1);
+    lbx_feed(st, f0, f1);
+  }
+  if (wv == 0 && lane == 0) {
+    const double wx = refmath::expit(st.x, obj.tb);
+    wnew[idx] = wx;
+    wdag[idx] = (wx > 0.5) ? sig1 : sig0;
+    if (info) {
+      const int nit = st.nit < 4095 ? st.nit : 4095;
+      const int nfev = st.nfev < 32767 ? st.nfev : 32767;
+      info[idx] = (int32_t)(st.status | (nit << 4) | (nfev << 16));
     }
   }
 }
@@ -588,8 +722,29 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   const int fin_blocks = d_ll1 ? (nchains + kExactWaves - 1) / kExactWaves : 0;
   const dim3 grid(lo_blocks + fin_blocks);
   // the latency form while the optima fit in two waves per SIMD (the GPU's
-  // 256 CUs x 4 SIMDs); the throughput form (four per SIMD) beyond
+  // 256 CUs x 4 SIMDs); the throughput form (four per SIMD) beyond; the pair
+  // form (option exact_form 3) for few optima with two slots or more
   const bool lat = c.exact_form == 1 || (c.exact_form == 0 && nw <= c.exact_lat_waves);
+  const bool pair = c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves));
+  if (pair) {
+    const int pfin = d_ll1 ? (nchains + 1) / 2 : 0;
+    const dim3 pgrid(nw + pfin);
+    switch (c.pw_ns) {
+#define NEMO_EXACT_PAIR(NSV)                                                                                     \
+  case NSV:                                                                                                      \
+    local_opt_exact_pair_kernel<NSV><<<pgrid, 2 * kWave, 0, st>>>(                                             \
+        c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
+        c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, nw, fin);                           \
+    break;
+      NEMO_EXACT_PAIR(2)
+      NEMO_EXACT_PAIR(3)
+      NEMO_EXACT_PAIR(4)
+#undef NEMO_EXACT_PAIR
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (c.pw_ns) {
 #define NEMO_EXACT_NS(NSV)                                                                                         \
   case NSV:                                                                                                        \

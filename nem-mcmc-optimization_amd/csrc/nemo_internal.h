@@ -114,10 +114,12 @@ struct Ctx {
   // calls (nemo_exact.hip): option "exact" (1 default), available when the
   // staged model is factored and numpy's pairwise sum of E fits the wave plan
   int exact = 1;
-  // the local-optimum kernel's form: 0 auto (latency form up to
-  // exact_lat_waves optima, throughput form beyond), 1 latency, 2 throughput
+  // the local-optimum kernel's form: 0 auto (pair form up to exact_pair_waves
+  // optima, latency form up to exact_lat_waves, throughput form beyond), 1
+  // latency, 2 throughput, 3 pair
   int exact_form = 0;
   int exact_lat_waves = 4096;
+  int exact_pair_waves = 0;
   bool exact_ok = false;
   double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
   double* d_xhi = nullptr;         // [S] numpy's exp(hi_j)

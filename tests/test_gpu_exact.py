@@ -92,6 +92,10 @@ def test_exact_scores_equal_reference_goldens(name, s, e):
     pos = np.array([np.argsort(p) for p in z["perm"]], dtype=np.int32)
     ll = eng.score(pos, expit(z["W"]))
     assert _bits_equal(ll, z["ll"])
+    # calculate_ll's column sums and order weights (nem_order_mcmc.py:89-93)
+    r = eng.score(pos, expit(z["W"]), want_cs=True, want_ow=True)
+    assert _bits_equal(r["ll"], z["ll"]) and _bits_equal(r["cs"], z["cs"])
+    assert _bits_equal(r["ow"][0], z["ow0"])
     eng.close()
 
 
@@ -114,6 +118,31 @@ def test_exact_fused_step_equals_oracle_c3():
     assert smp.ll == ora.ll1
     assert _bits_equal(smp.parent_weights, ora.w)
     assert got_dag == ref_dag
+    eng.close()
+
+
+def test_exact_kernel_forms_give_the_same_bits():
+    """The local-optimum kernel's latency, throughput and pair forms (option
+    exact_form 1 / 2 / 3): the same weights, dag weights and lls, to the bit,
+    for one chain and for three."""
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(4)
+    for n in (1, 3):
+        pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
+        w = rng.uniform(-3, 3, (n, 64, 64))
+        anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
+        outs = []
+        for form in (1, 2, 3):
+            eng.set_option("exact_form", form)
+            r = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
+            outs.append([np.array(x, copy=True) for x in r])
+        for o in outs[1:]:
+            assert len(o) == len(outs[0])
+            for a, b in zip(outs[0], o):
+                assert _bits_equal(a, b)
+    eng.set_option("exact_form", 0)
     eng.close()
 
 

@@ -108,8 +108,8 @@ done
 task_exact_form() (
 P=${PROF_DIR:-gpurun_out/exact_form}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
 NO_AB=1 TESTS="${TESTS:-exact or raises}" bash tools/gpu_tasks.sh exact || exit 1
-for n in 1 4 16; do
-  timeout -k 10 180 env AB_OPT=exact_form AB_VALS=1,2 python tools/step_probe.py $n > "$P/n$n.log" 2>&1 || { tail "$P/n$n.log"; exit 1; }
+for n in ${CHAINS:-1 2 4 16}; do
+  timeout -k 10 180 env AB_OPT=exact_form AB_VALS=${FORMS:-1,2,3} python tools/step_probe.py $n > "$P/n$n.log" 2>&1 || { tail "$P/n$n.log"; exit 1; }
   echo "n=$n"; grep "^AB" "$P/n$n.log"
 done
 )

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kExactWaves * kWave) void obj_bench_kernel(int W, i
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (gw >= W) return;
-  using Obj = ExactObjective<NS, true>;
+  using Obj = ExactObjective<NS, true, false>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
