@@ -253,10 +253,12 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                tables, no parent cap, numpy's pairwise sum of E fits the
  *                wave plan)
  *   "exact_form" the exact local-optimum kernel's form (same bits): 0 auto
- *                (default: latency form while chains x pairs <=
- *                "exact_lat_waves", 4096 by default, throughput form beyond),
- *                1 latency (two waves per SIMD, a slot's c loaded at once),
- *                2 throughput (four waves per SIMD) */
+ *                (default: pair form while chains x pairs <= "exact_pair_waves",
+ *                16384 by default, then the latency form up to
+ *                "exact_lat_waves" (0), the throughput form beyond), 1 latency
+ *                (one wave per optimum, two per SIMD), 2 throughput (four per
+ *                SIMD), 3 pair (two waves per optimum, the objective's slots
+ *                split between them; E > 1024) */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

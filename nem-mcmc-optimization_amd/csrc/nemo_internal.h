@@ -115,11 +115,12 @@ struct Ctx {
   // staged model is factored and numpy's pairwise sum of E fits the wave plan
   int exact = 1;
   // the local-optimum kernel's form: 0 auto (pair form up to exact_pair_waves
-  // optima, latency form up to exact_lat_waves, throughput form beyond), 1
+  // optima -- measured best from 1 to 4 C3 chains, level at 16 -- then the
+  // latency form up to exact_lat_waves, the throughput form beyond), 1
   // latency, 2 throughput, 3 pair
   int exact_form = 0;
-  int exact_lat_waves = 4096;
-  int exact_pair_waves = 0;
+  int exact_lat_waves = 0;
+  int exact_pair_waves = 16384;
   bool exact_ok = false;
   double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
   double* d_xhi = nullptr;         // [S] numpy's exp(hi_j)

@@ -51,12 +51,13 @@ NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c
 
 // svml_log's reduction row for n = the number of vrcp14 switch points at or
 // below the mantissa (kRcp14Switch): r = RNE_1/32(vrcp14pd(m)) = (32 - n) / 32,
-// the exponent adjustment (1 when r < 0.75) and T(r) = log_hi + log_lo
+// the exponent adjustment (1 when r < 0.75) minus the exponent bias 1023, and
+// T(r) = log_hi + log_lo
 NEMO_RM void svml_log_row(int n, double* row) {
   const double r = (double)(32 - n) * 0.03125;
   const int j = (int)(as_u64(r) >> 48) & 15;
   row[0] = r;
-  row[1] = r < 0.75 ? 1.0 : 0.0;
+  row[1] = (r < 0.75 ? 1.0 : 0.0) - 1023.0;   // the exponent's adjustment and its bias, exact
   row[2] = as_double(kSvmlLogHi[j]);
   row[3] = as_double(kSvmlLogLo[j]);
 }
@@ -338,7 +339,7 @@ NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   const uint32_t p22 = (uint32_t)(b >> 30) & 0x3fffff;
   double r, kadj, thi, tlo;
   tb.log_row(p22, r, kadj, thi, tlo);
-  const double k = (double)((int)((b >> 52) & 0x7ff) - 1023) + kadj;   // + 1 when r < 0.75
+  const double k = (double)(int)((b >> 52) & 0x7ff) + kadj;   // e - 1023, + 1 when r < 0.75
   const double R = fma_(r, m, -1.0);
   double p7 = fma_(R, C200, C240);
   double p1 = fma_(R, C180, C1c0);
