@@ -336,9 +336,9 @@ NEMO_LB int formt(Mem& mem, const Ring& rg, double theta, Lanes L) {
   double* wt = mem.wt();
   auto sy = [&](int i, int k) { return i == k ? mem.syd(i) : prod0(mem.ws(i), mem.wy(k)); };
   auto ss = [&](int i, int k) { return i == k ? mem.ssd(i) : prod0(mem.ws(i), mem.ws(k)); };
-  for (int t = L.id; t < kM * kM; t += L.n) {
+  for (int t = L.id; t < kM * col; t += L.n) {
     const int i = t % kM, j = t / kM;
-    if (j >= col || i > j) continue;
+    if (i > j) continue;
     if (i == 0) {
       wt[(long)j * kLdT] = theta * ss(0, j);
     } else {
@@ -360,9 +360,9 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
   const int col = rg.col, c2 = 2 * col;
   double* wn = mem.wn();
   auto at = [&](int r, int c) -> double& { return wn[r + (long)c * kLdN]; };
-  for (int t = L.id; t < kLdN * kLdN; t += L.n) {
+  for (int t = L.id; t < kLdN * c2; t += L.n) {
     const int r = t % kLdN, c = t / kLdN;
-    if (c >= c2 || r > c) continue;
+    if (r > c) continue;
     double v;
     if (c < col) {            // Y'ZZ'Y / theta, + s'y on the diagonal
       v = sum0(mem.wy(c), mem.wy(r)) / theta;
@@ -381,9 +381,9 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
   double* b12 = wn + (long)col * kLdN;
   const int info = col == 1 ? ob_trsv_tun(1, wn, kLdN, b12) : ob_trsm_lt(col, col, wn, kLdN, b12, kLdN, L);
   if (info != 0) return -1;
-  for (int t = L.id; t < kM * kM; t += L.n) {
+  for (int t = L.id; t < kM * col; t += L.n) {
     const int a = t % kM, b = t / kM;
-    if (b >= col || a > b) continue;
+    if (a > b) continue;
     const int is = col + a, js = col + b;
     at(is, js) = at(is, js) + ob_ddot(col, wn + (long)is * kLdN, wn + (long)js * kLdN);
   }
