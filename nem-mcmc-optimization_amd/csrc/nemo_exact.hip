@@ -265,15 +265,18 @@ struct ExactObjective {
     const int cu = cnt(u);
     a0 = 0.0;
     a1 = 0.0;
+    // past the chain's count c is 0 (the rows are written so; cval gives 0),
+    // so its term is log(0 ex + 1) = +0 and a + 0 = a: a is never -0 (a log is
+    // never -0, and a sum of nonzero terms rounds to +0), so no select is needed
     auto step = [&](int m, double cm) {
       const double t0 = refmath::svml_log(cm * ex0 + 1.0, tb);
       const double t1 = refmath::svml_log(cm * ex1 + 1.0, tb);
       if (m == 0) {
-        a0 = cu > 0 ? t0 : 0.0;
-        a1 = cu > 0 ? t1 : 0.0;
+        a0 = t0;
+        a1 = t1;
       } else {
-        a0 = m < cu ? a0 + t0 : a0;
-        a1 = m < cu ? a1 + t1 : a1;
+        a0 = a0 + t0;
+        a1 = a1 + t1;
       }
     };
     if (kLat) {

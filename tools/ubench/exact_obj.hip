@@ -10,14 +10,17 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
-// per-part cycle totals of the control (lane 0 of every wave adds its own)
+// per-part cycle totals of the control (lane 0 of every wave adds its own;
+// -DNEMO_UB_NOHOOK: the plain control, for its time)
 __device__ unsigned long long g_lbx_t[8];
+#ifndef NEMO_UB_NOHOOK
 #define NEMO_LBX_T(k, stmt)                                                              \
   do {                                                                                   \
     const long long t0_ = clock64();                                                     \
     stmt;                                                                                \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_lbx_t[k], (unsigned long long)(clock64() - t0_)); \
   } while (0)
+#endif
 #include "nemo_exact.hip"
 
 namespace nemo {
