@@ -633,6 +633,13 @@ def main():
             t0 = time.perf_counter()
             eng.score(pos[:1], w01[:1], cap=cap)
             lat.append(time.perf_counter() - t0)
+        eng.set_option("exact", 0)
+        lat_fast = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            eng.score(pos[:1], w01[:1], cap=cap)
+            lat_fast.append(time.perf_counter() - t0)
+        eng.set_option("exact", 1)
         ts1 = []
         for _ in range(20):
             t0 = time.perf_counter()
@@ -643,6 +650,8 @@ def main():
             "score_call_us": 1e6 * float(np.median(lat)), "evals_per_s_sequential": 1.0 / float(np.median(lat)),
             "fused_step_ms": 1e3 * float(np.median(ts1)), "chain_steps_per_s": 1.0 / float(np.median(ts1)),
             "fused_step_ms_fast_kernels": 1e3 * fs1_fast,
+            "score_call_us_fast_kernels": 1e6 * float(np.median(lat_fast)),
+            "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
             "reference_cpu_s_per_chain_step": 1.2,
             "includes": "score_call_us: one synchronous nemo_score call for one (pos, W) from host "
                         "arrays; fused_step_ms: nemo_optimal_weights for one chain (eval#1 with order "
