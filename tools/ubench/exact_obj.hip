@@ -14,11 +14,13 @@
 // -DNEMO_UB_NOHOOK: the plain control, for its time)
 __device__ unsigned long long g_lbx_t[8];
 #ifndef NEMO_UB_NOHOOK
+// per-wave totals in LDS (lane 0 adds; one global atomic per wave at the end)
+__shared__ unsigned long long ub_t[4][8];
 #define NEMO_LBX_T(k, stmt)                                                              \
   do {                                                                                   \
-    const long long t0_ = clock64();                                                     \
+    const long long t0_ = wall_clock64();                                                \
     stmt;                                                                                \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_lbx_t[k], (unsigned long long)(clock64() - t0_)); \
+    if ((threadIdx.x & 63) == 0) ub_t[threadIdx.x >> 6][k] += (unsigned long long)(wall_clock64() - t0_); \
   } while (0)
 #endif
 #include "nemo_exact.hip"
@@ -82,6 +84,9 @@ __global__ __launch_bounds__(kExactWaves * kWave) void ctrl_bench_kernel(int W, 
   const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   if (gw >= W) return;
   CheapObjective obj{prm[3 * gw], prm[3 * gw + 1], 40.0, tabs.view()};
+#ifndef NEMO_UB_NOHOOK
+  if ((threadIdx.x & 63) < 8) ub_t[wv][threadIdx.x & 63] = 0;
+#endif
   LbxState reg;
   LbxState& st = kLds ? *reinterpret_cast<LbxState*>(lst_raw[wv]) : reg;
   lbx_init(st, prm[3 * gw + 2]);
@@ -96,6 +101,9 @@ __global__ __launch_bounds__(kExactWaves * kWave) void ctrl_bench_kernel(int W, 
   if ((threadIdx.x & (kWave - 1)) == 0) {
     out[2 * gw] = st.x;
     out[2 * gw + 1] = st.nfev;
+#ifndef NEMO_UB_NOHOOK
+    for (int q = 0; q < 8; ++q) atomicAdd(&g_lbx_t[q], ub_t[wv][q]);
+#endif
   }
 }
 
@@ -184,7 +192,7 @@ int main(int argc, char** argv) {
       const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_lbx_t), z, sizeof(z)));
       const char* nm[6] = {"dcsrch", "formt", "formk", "subsm", "lbx_run", "objective"};
-      printf("   cycles per wave:");
+      printf("   wall-clock (100 MHz) ticks per wave:");
       for (int k = 0; k < 6; ++k) printf(" %s %.0f", nm[k], (double)t[k] / W);
       printf("\n");
     }
