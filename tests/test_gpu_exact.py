@@ -121,6 +121,32 @@ def test_exact_fused_step_equals_oracle_c3():
     eng.close()
 
 
+@pytest.mark.parametrize("e", [2600, 4096])
+def test_exact_fused_step_equals_oracle_more_slots(e):
+    """E past 2048 (32 leaves of 128: four slots of the wave plan): one fused step in
+    the throughput and the pair forms against the oracle, to the bit."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(12, e, 3)
+    eng = Engine.for_nem(m)
+    assert eng.get_option("exact_ok") == 1
+    t = m.get_score_tensor()
+    rng = np.random.default_rng(e)
+    perm = rng.permutation(m.num_s)
+    w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
+    ora = no.OracleSampler(m.U, t, perm)
+    ora.w = w_raw.copy()
+    ref_dag = ora.optimal_weights()
+    for form in (2, 3):
+        eng.set_option("exact_form", form)
+        smp = NEMOrderMCMC(m, perm, engine=eng)
+        smp.parent_weights = w_raw.copy()
+        got_dag = smp.get_optimal_weights(init=True)
+        assert smp.ll == ora.ll1 and got_dag == ref_dag, form
+        assert _bits_equal(smp.parent_weights, ora.w), form
+    eng.set_option("exact_form", 0)
+    eng.close()
+
+
 def test_exact_kernel_forms_give_the_same_bits():
     """The local-optimum kernel's latency, throughput and pair forms (option
     exact_form 1 / 2 / 3): the same weights, dag weights and lls, to the bit,
