@@ -453,6 +453,31 @@ def c3_fp64(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, ll_ref, steps=
     return out
 
 
+def c3_exact(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, pos, w01, ll_ref, steps=5, warmup_s=0.3):
+    """The headline workload (same model, same resident inputs, same B) in
+    the reference's own arithmetic (option exact_dev: numpy's SVML log / exp,
+    glibc's exp / log1p in logaddexp.reduce, Python's left fold; the
+    nemo_exact.hip kernels), with its first evaluations checked bit for bit
+    against the host-pointer exact path."""
+    d_ll = torch.zeros(B, dtype=torch.float64, device="cuda")
+    eng.set_option("exact_dev", 1)
+    try:
+        wall, kms, _ = timed_steps(eng, torch, B, cap, steps, 1, d_pos, d_w01, d_ll, stream, 1, dist,
+                                   warmup_s=warmup_s)
+    finally:
+        eng.set_option("exact_dev", 0)
+    got = d_ll.cpu().numpy()
+    nchk = min(B, 8)
+    host = eng.score(pos[:nchk], w01[:nchk], cap=cap)
+    return {"workload": f"C3: S={S} E={E}, {B} evaluations per launch, the reference's arithmetic (bits of "
+                        "numpy's calculate_ll)",
+            "kernels": "exact_cells_kernel, exact_fold_kernel, exact_seq_sum_kernel (nemo_exact.hip)",
+            "evals_per_s": B * steps / wall, "kernel_avg_ms": kms,
+            "bits_equal_host_exact_first": int(nchk) if np.array_equal(got[:nchk].view(np.uint64),
+                                                                       host.view(np.uint64)) else 0,
+            "max_abs_ll_diff_vs_headline": float(np.max(np.abs(got - ll_ref)))}
+
+
 def wide_uncapped(torch, dist, stream, batch=2048, steps=5, warmup_s=0.3):
     """Uncapped 64 < S <= 128 (generator config W128: 128 x 2000): the int8
     log2 kernel for wide models (fact_kernel 18, what auto takes within the
@@ -592,6 +617,9 @@ def main():
             # the same workload in fp64 arithmetic (the headline's dtype is fixed point)
             extras["c3_fp64"] = c3_fp64(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, ll,
                                         warmup_s=min(args.warmup_seconds, 0.3))
+            if eng.get_option("exact_ok"):
+                extras["c3_exact"] = c3_exact(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, pos, w01, ll,
+                                              warmup_s=min(args.warmup_seconds, 0.3))
         # fused per-step scorer of the sampler: 16 chains (C4 share of one GPU)
         from nemo.nem_order_mcmc import SIG0, SIG1
         nch = 16

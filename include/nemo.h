@@ -249,6 +249,10 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                the same order scores, order weights, local optima and
  *                weights as nem_order_mcmc.py, to the bit, when "exact_ok";
  *                0 = the fast kernels (scores within ~1e-9)
+ *   "exact_dev"  0 (default): nemo_score_dev runs the fast kernels; 1 = the
+ *                same conditions as "exact" on nemo_score, on device buffers
+ *                (cells built in d_ow -- then order weights in place -- or in
+ *                d_cells, not both)
  *   "exact_ok"   (get only) 1 if the staging supports "exact" (factored
  *                tables, no parent cap, numpy's pairwise sum of E fits the
  *                wave plan)

@@ -36,6 +36,8 @@ struct nemo_ctx {
   // submission order; the caller collects them in the same order
   // (nemo_host.h StepQueue; created on the first _begin)
   std::unique_ptr<nemo::host::StepQueue<StepJob>> steps;
+  // option "exact_dev": nemo_score_dev in the reference's arithmetic
+  int exact_dev = 0;
 };
 
 namespace {
@@ -491,6 +493,17 @@ int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double*
   hipStream_t st = pick(ctx, stream);
   if (c.score_path == 2 && !c.factored)
     return fail(NEMO_ERR_STATE, "score_path=2 (factored) but the staged table is not factorable");
+  if (ctx->exact_dev && use_factored(c) && c.fact_kernel == 0 && (cap == 0 || cap >= (int)c.S - 1) &&
+      nemo::exact_supported(c)) {
+    // nemo_score's exact path on device buffers: the cells are built in the
+    // caller's d_ow (turned into order weights in place) or d_cells, else in
+    // the context's scratch
+    if (d_cells && d_ow) return fail(NEMO_ERR_ARG, "exact_dev: cells and order weights share one buffer");
+    double* cells = d_ow ? d_ow : d_cells ? d_cells : c.d_ow;
+    HIPCHK(nemo::launch_exact_eval(c, batch, d_pos, d_w01, cells, d_cs ? d_cs : c.d_cs, d_ll, d_ow != nullptr, st));
+    if (cells == c.d_ow) c.ow_chains = 0;  // d_ow no longer holds fused-step order weights
+    return NEMO_OK;
+  }
   if (use_factored(c)) {
     HIPCHK(nemo::launch_score_factored(c, batch, cap, d_pos, d_w01, d_ll, d_cs, d_cells, d_ow, st));
     return NEMO_OK;
@@ -1171,6 +1184,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.exact = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "exact_dev") == 0) {
+    ctx->exact_dev = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "exact_form") == 0) {
     if (value < 0 || value > 3)
       return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair)", value);
@@ -1243,6 +1260,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "local_split") == 0) *value = c.local_split;
   else if (strcmp(name, "graphs") == 0) *value = c.graphs;
   else if (strcmp(name, "exact") == 0) *value = c.exact;
+  else if (strcmp(name, "exact_dev") == 0) *value = ctx->exact_dev;
   else if (strcmp(name, "exact_form") == 0) *value = c.exact_form;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;

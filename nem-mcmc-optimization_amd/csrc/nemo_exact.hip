@@ -46,6 +46,22 @@ struct TabsLds {
     }
     for (int q = t; q < 256; q += nt) gexp[q] = refmath::kGlibcExpTab[q];
   }
+  // only what svml_log reads
+  __device__ void fill_log(int t, int nt) {
+    for (int q = t; q < 128; q += nt) refmath::svml_log_row((int)refmath::kRcp14Base[q >> 1] + (q & 1), lrow[q]);
+    for (int q = t; q < 64; q += nt) rthr[q] = refmath::kRcp14InBucket[q];
+  }
+  // only what glibc_exp reads (logaddexp)
+  __device__ void fill_gexp(int t, int nt) {
+    for (int q = t; q < 256; q += nt) gexp[q] = refmath::kGlibcExpTab[q];
+  }
+  // only what svml_exp reads
+  __device__ void fill_exp(int t, int nt) {
+    for (int q = t; q < 16; q += nt) {
+      erow[q][0] = refmath::as_double(refmath::kSvmlExpHi[q]);
+      erow[q][1] = refmath::as_double(refmath::kSvmlExpLo[q]);
+    }
+  }
   __device__ LdsTabs view() const { return LdsTabs{rthr, &lrow[0][0], &erow[0][0], gexp}; }
 };
 
@@ -54,33 +70,37 @@ __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nword
 }
 
 // ---------------------------------------------------------------------------
-// cells: one block per (evaluation, child i, 256 effects).  The block first
-// evaluates the child's two log factors per parent, log((1 - s) + s x) for x =
-// exp(lo_j), exp(hi_j) (numpy: `1.0 - expit(w) + expit(w) * np.exp(T)`, then
-// np.log), then each thread adds them to U[i][e] in pi's parent order.  Row S
+// cells: one block per (evaluation, child i).  The block first evaluates the
+// child's two log factors per parent, log((1 - s) + s x) for x = exp(lo_j),
+// exp(hi_j) (numpy: `1.0 - expit(w) + expit(w) * np.exp(T)`, then np.log),
+// then each thread adds them to U[i][e] in pi's parent order.  Row S
 // (attached to nothing) is U[S].  Cells go to `cells` [b][S+1][E].
+// A wave covers the 64 effects of one D1 word at a time, so a parent's word
+// is one scalar load and its bits are the wave's lane mask (inverse ballot)
+// choosing between the parent's two factors.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void exact_cells_kernel(int S, int E, int etiles, const int32_t* __restrict__ pos,
-                                                          const double* __restrict__ w01,
-                                                          const double* __restrict__ xlo,
-                                                          const double* __restrict__ xhi,
-                                                          const uint64_t* __restrict__ d1w, int nwords,
-                                                          const double* __restrict__ U, double* __restrict__ cells) {
+constexpr int kCellsThreads = 512;
+
+__global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E, const int32_t* __restrict__ pos,
+                                                                    const double* __restrict__ w01,
+                                                                    const double* __restrict__ xlo,
+                                                                    const double* __restrict__ xhi,
+                                                                    const uint64_t* __restrict__ d1w, int nwords,
+                                                                    const double* __restrict__ U,
+                                                                    double* __restrict__ cells) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ int perm[kMaxS];
   __shared__ double v[kMaxS][2];
-  const int et = blockIdx.x % etiles;
-  const int i = (blockIdx.x / etiles) % (S + 1);
-  const int b = blockIdx.x / (etiles * (S + 1));
+  const int i = blockIdx.x % (S + 1);
+  const int b = blockIdx.x / (S + 1);
   const int t = threadIdx.x;
-  const int e = et * 256 + t;
-  tabs.fill(t, blockDim.x);
   const int32_t* pb = pos + (size_t)b * S;
+  const int pi = i < S ? pb[i] : 0;
+  if (pi > 0) tabs.fill_log(t, blockDim.x);
   for (int q = t; q < S; q += blockDim.x) perm[pb[q]] = q;
   __syncthreads();
   const LdsTabs tb = tabs.view();
-  const int pi = i < S ? pb[i] : 0;
   for (int q = t; q < pi; q += blockDim.x) {
     const int j = perm[q];
     const double s = w01[((size_t)b * S + i) * S + j];
@@ -89,10 +109,31 @@ __global__ __launch_bounds__(256) void exact_cells_kernel(int S, int E, int etil
     v[q][1] = refmath::svml_log(oms + s * xhi[j], tb);
   }
   __syncthreads();
-  if (e >= E) return;
-  double cell = U[(size_t)i * E + e];
-  for (int q = 0; q < pi; ++q) cell = cell + v[q][d1bit(d1w, nwords, perm[q], e)];
-  cells[((size_t)b * (S + 1) + i) * E + e] = cell;
+  const int lane = t & (kWave - 1);
+  const double* urow = U + (size_t)i * E;
+  double* crow = cells + ((size_t)b * (S + 1) + i) * E;
+  constexpr int kU = 8;  // parents per batch of loads ahead of their adds
+  for (int word = __builtin_amdgcn_readfirstlane(t / kWave); word * kWave < E; word += kCellsThreads / kWave) {
+    const int e = word * kWave + lane;
+    double cell = e < E ? urow[e] : 0.0;
+    const uint64_t* dw = d1w + word;
+    int q = 0;
+    for (; q + kU <= pi; q += kU) {
+      uint64_t wd[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) wd[u] = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords];
+      double f[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) f[u] = v[q + u][__builtin_amdgcn_inverse_ballot_w64(wd[u]) ? 1 : 0];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) cell = cell + f[u];
+    }
+    for (; q < pi; ++q) {
+      const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords];
+      cell = cell + v[q][__builtin_amdgcn_inverse_ballot_w64(wd) ? 1 : 0];
+    }
+    if (e < E) crow[e] = cell;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -107,7 +148,7 @@ __global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch
                                                          double* __restrict__ cs) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
-  tabs.fill(threadIdx.x, blockDim.x);
+  tabs.fill_gexp(threadIdx.x, blockDim.x);
   __syncthreads();
   const LdsTabs tb = tabs.view();
   const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -143,7 +184,7 @@ __global__ __launch_bounds__(256) void exact_ow_kernel(int S, int E, int batch, 
                                                        const double* __restrict__ cs) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
-  tabs.fill(threadIdx.x, blockDim.x);
+  tabs.fill_exp(threadIdx.x, blockDim.x);
   __syncthreads();
   const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   const size_t n = (size_t)batch * (S + 1) * E;
@@ -695,9 +736,8 @@ size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjecti
 hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
   const int S = c.S, E = c.E;
-  const int etiles = (E + 255) / 256;
-  exact_cells_kernel<<<dim3(batch * (S + 1) * etiles), 256, 0, st>>>(S, E, etiles, d_pos, d_w01, c.d_xlo, c.d_xhi,
-                                                                     c.d_D1w, c.nwords, c.d_U64, d_cells);
+  exact_cells_kernel<<<dim3(batch * (S + 1)), kCellsThreads, 0, st>>>(S, E, d_pos, d_w01, c.d_xlo, c.d_xhi, c.d_D1w,
+                                                                      c.nwords, c.d_U64, d_cells);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   const size_t nthr = (size_t)batch * E;

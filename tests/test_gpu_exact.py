@@ -99,6 +99,49 @@ def test_exact_scores_equal_reference_goldens(name, s, e):
     eng.close()
 
 
+def test_exact_score_dev_equals_reference_goldens():
+    """Option exact_dev: the batched device entry in the reference's
+    arithmetic -- the golden ll, cs and order weights to the bit, and the
+    host-pointer exact path's bits at a batch of 300."""
+    import torch
+    z = golden("eval_C3.npz")
+    m = generator.synthetic_nem(64, 2000, 0)
+    eng = Engine.for_nem(m)
+    eng.set_option("exact_dev", 1)
+    assert eng.get_option("exact_dev") == 1
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    s, e = 64, 2000
+
+    def run(pos, w01, extras):
+        b = pos.shape[0]
+        eng.reserve(b)
+        dpos = torch.from_numpy(pos).cuda()
+        dw = torch.from_numpy(w01).cuda()
+        dll = torch.zeros(b, dtype=torch.float64, device="cuda")
+        dcs = torch.zeros((b, e), dtype=torch.float64, device="cuda") if extras else None
+        dow = torch.zeros((b, s + 1, e), dtype=torch.float64, device="cuda") if extras else None
+        _lib.check(lib.nemo_score_dev(eng._ctx, b, dpos.data_ptr(), dw.data_ptr(), 0, dll.data_ptr(),
+                                      dcs.data_ptr() if extras else None, None,
+                                      dow.data_ptr() if extras else None, st))
+        torch.cuda.synchronize()
+        return dll.cpu().numpy(), (dcs.cpu().numpy() if extras else None), (dow.cpu().numpy() if extras else None)
+
+    pos = np.array([np.argsort(p) for p in z["perm"]], dtype=np.int32)
+    w01 = expit(z["W"])
+    ll, cs, ow = run(pos, w01, True)
+    assert _bits_equal(ll, z["ll"]) and _bits_equal(cs, z["cs"]) and _bits_equal(ow[0], z["ow0"])
+    rng = np.random.default_rng(9)
+    pos = np.array([rng.permutation(s) for _ in range(300)], dtype=np.int32)
+    w01 = expit(rng.uniform(-6, 6, (300, s, s)))
+    ll, _, _ = run(pos, w01, False)
+    assert _bits_equal(ll, eng.score(pos, w01))
+    eng.set_option("exact_dev", 0)   # the fast kernels again: within 1e-6, not the same bits
+    ll_fast, _, _ = run(pos, w01, False)
+    assert np.max(np.abs(ll_fast - ll)) <= 1e-6
+    eng.close()
+
+
 def test_exact_fused_step_equals_oracle_c3():
     """One get_optimal_weights at 64 x 2000 (2016 local optima) against the
     oracle, i.e. numpy and scipy: every weight, ll and dag_ll to the bit."""

@@ -184,6 +184,24 @@ TAILN=3 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "
 cut -c1-160 "$P"/trace/*kernel_stats.csv | head -12
 )
 
+# ---- exact_dev: batched order scores in the reference's arithmetic (option exact_dev):
+# the GPU test, tools/exact_score_probe.py (ms per call by batch, bits against the host
+# exact path), and its kernel trace
+task_exact_dev() (
+P=${PROF_DIR:-gpurun_out/exact_dev}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$P/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -${TAILN:-4} "$P/$name.log"; return $rc; }
+TAILN=6 step tests 600 python -u -m pytest tests/test_gpu_exact.py -k "${TESTS:-score_dev or scores_equal}" -v --timeout 300 --timeout-method thread || exit 1
+TAILN=6 step probe 300 python tools/exact_score_probe.py ${SIZES:-16 128 2048} || exit 1
+if [ -f nem-mcmc-optimization_amd/nemo/libnemo_old.so ]; then   # interleaved A/B against another build
+  for r in $(seq ${ROUNDS:-2}); do
+    TAILN=3 step "probe_old_$r" 300 env NEMO_LIBRARY=$R/nem-mcmc-optimization_amd/nemo/libnemo_old.so python tools/exact_score_probe.py ${SIZES:-16 128 2048} || exit 1
+    TAILN=3 step "probe_new_$r" 300 python tools/exact_score_probe.py ${SIZES:-16 128 2048} || exit 1
+  done
+fi
+TAILN=2 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$P/trace" -o t -- python "$R/tools/exact_score_probe.py" ${SIZES:-16 128 2048} || exit 1
+cut -c1-140 "$P/trace/t_kernel_stats.csv" | head -8
+)
+
 # ---- step_trace: kernel trace of the fused step for 1 and 16 chains (tools/step_probe.py)
 task_step_trace() (
 P=${PROF_DIR:-gpurun_out/step_trace}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -194,6 +212,6 @@ done
 )
 
 case "$task" in
-  ab|ab_step|batch|c4_rehearsal|exact|exact_ab|exact_form|exact_prof|lo|prof|small|split|step_trace) "task_$task" "$@" ;;
-  *) echo "tasks: ab ab_step batch c4_rehearsal exact exact_ab exact_form exact_prof lo prof small split step_trace"; exit 2 ;;
+  ab|ab_step|batch|c4_rehearsal|exact|exact_ab|exact_dev|exact_form|exact_prof|lo|prof|small|split|step_trace) "task_$task" "$@" ;;
+  *) echo "tasks: ab ab_step batch c4_rehearsal exact exact_ab exact_dev exact_form exact_prof lo prof small split step_trace"; exit 2 ;;
 esac
