@@ -285,7 +285,8 @@ int nemo_set_option_f64(nemo_ctx* ctx, const char* name, double value);
 /* Test hook: refmath.h's restatements evaluated on the current device, for
  * the tests that compare them with numpy / scipy bit for bit.  fn: 0 np.log
  * (SVML), 1 np.exp (SVML), 2 scipy.special.expit, 3 np.logaddexp(x, y),
- * 4 glibc exp, 5 glibc log1p, 6 sqrt, 7 x / y (the optimiser's IEEE operations).
+ * 4 glibc exp, 5 glibc log1p, 6 sqrt, 7 x / y (the optimiser's IEEE operations),
+ * 8 glibc log1p on [0, 1] as logaddexp evaluates it.
  * Host arrays of n doubles (y only for fn 3 and 7). */
 int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out);
 int nemo_get_option_f64(nemo_ctx* ctx, const char* name, double* value);

@@ -1273,7 +1273,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
 }
 
 int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out) {
-  if (n < 0 || fn < 0 || fn > 7 || (n > 0 && (!x || !out || ((fn == 3 || fn == 7) && !y))))
+  if (n < 0 || fn < 0 || fn > 8 || (n > 0 && (!x || !out || ((fn == 3 || fn == 7) && !y))))
     return fail(NEMO_ERR_ARG, "fn=%d n=%d / null pointer", fn, n);
   if (n == 0) return NEMO_OK;
   int ndev = 0;

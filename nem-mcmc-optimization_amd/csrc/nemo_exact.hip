@@ -696,7 +696,9 @@ __global__ void refmath_probe_kernel(int fn, int n, const double* __restrict__ x
     case 4: r = refmath::glibc_exp(v, tb); break;
     case 5: r = refmath::glibc_log1p(v); break;
     case 6: r = __builtin_sqrt(v); break;  // the optimiser's square roots and divisions
-    default: r = v / y[g]; break;
+    case 7: r = v / y[g]; break;
+    case 8: r = refmath::log1p_unit(v); break;
+    default: r = v; break;
   }
   out[g] = r;
 }

@@ -49,6 +49,25 @@ NEMO_RM double as_double(uint64_t u) { return __builtin_bit_cast(double, u); }
 NEMO_RM uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
 NEMO_RM double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// n / d rounded to nearest, for d in [1, 4) and n = 0 or |n| in [2^-60, 4):
+// on the device the core of the compiler's division sequence (reciprocal,
+// two Newton steps, the residual correction) without v_div_scale /
+// v_div_fmas's scaling and v_div_fixup's special cases, which leave such
+// operands unchanged -- the same bits as `n / d` in three fewer instructions
+// (tests/test_gpu_exact.py).  A smaller |n| (the residual would lose bits)
+// still gives a finite value near n / d.  On the host n / d
+NEMO_RM double div_rn(double n, double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y0 = __builtin_amdgcn_rcp(d);
+  const double y1 = __builtin_fma(y0, __builtin_fma(-d, y0, 1.0), y0);
+  const double y = __builtin_fma(y1, __builtin_fma(-d, y1, 1.0), y1);
+  const double q = n * y;
+  return __builtin_fma(__builtin_fma(-d, q, n), y, q);
+#else
+  return n / d;
+#endif
+}
+
 // svml_log's reduction row for n = the number of vrcp14 switch points at or
 // below the mantissa (kRcp14Switch): r = RNE_1/32(vrcp14pd(m)) = (32 - n) / 32,
 // the exponent adjustment (1 when r < 0.75) minus the exponent bias 1023, and
@@ -249,12 +268,13 @@ NEMO_RM double glibc_log1p(double x) {
   return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
 }
 
-// glibc_log1p for x in [0, 1] (logaddexp's argument exp(-|x - y|)) without
-// branches on the common paths: the k = 0 branch (x < 0.41422) and the
-// normalising branch (x >= 0.41422, one more division) computed together and
-// selected per lane -- in a wave whose lanes take both, the branchy form runs
-// both anyway.  The tiny and |f| < 2^-20 cases stay branches (rare).  Same
-// bits as glibc_log1p on [0, 1] (tests/host/refmath_check.cpp).
+// glibc_log1p for x in [0, 1] (logaddexp's argument exp(-|x - y|)) with one
+// path for most lanes: x < 0.41422 (k = 0, f = x) is the default, the
+// normalising branch (x >= 0.41422: 1 + x split into 2^k u and its rounding
+// error c, one more division) and the k != 0 form run only in waves with a
+// lane that needs them, and both divisions are div_rn.  The tiny and |f| <
+// 2^-20 cases stay branches (rare).  Same bits as glibc_log1p on [0, 1]
+// (tests/host/refmath_check.cpp, tests/test_gpu_exact.py).
 NEMO_RM double log1p_unit(double x) {
   NEMO_RM_NOCONTRACT
   constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
@@ -263,33 +283,32 @@ NEMO_RM double log1p_unit(double x) {
                    Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
                    Lp7 = 1.479819860511658591e-01;
   const int32_t hx = (int32_t)(as_u64(x) >> 32);
-  // x >= 0.41422: u = 1 + x normalised to [sqrt(2)/2, sqrt(2)), k its exponent
-  const double u = 1.0 + x;
-  const int32_t hu0 = (int32_t)(as_u64(u) >> 32);
-  int32_t kb = (hu0 >> 20) - 1023;
-  double cb = kb > 0 ? 1.0 - (u - x) : x - (u - 1.0);
-  cb = cb / u;
-  int32_t hum = hu0 & 0x000fffff;
-  const bool up = hum >= 0x6a09e;
-  const uint64_t lo = as_u64(u) & 0xffffffffull;
-  const double un = as_double(((uint64_t)(uint32_t)(hum | (up ? 0x3fe00000 : 0x3ff00000)) << 32) | lo);
-  kb = up ? kb + 1 : kb;
-  hum = up ? (0x00100000 - hum) >> 2 : hum;
-  const bool big = hx >= 0x3FDA827A;
-  const double f = big ? un - 1.0 : x;
-  const int32_t k = big ? kb : 0;
-  const double c = big ? cb : 0.0;
-  const int32_t hu = big ? hum : 1;
+  double f = x, c = 0.0;
+  int32_t k = 0, hu = 1;
+  if (hx >= 0x3FDA827A) {
+    // u = 1 + x normalised to [sqrt(2)/2, sqrt(2)), k its exponent
+    const double u = 1.0 + x;
+    const int32_t hu0 = (int32_t)(as_u64(u) >> 32);
+    k = (hu0 >> 20) - 1023;
+    c = div_rn(k > 0 ? 1.0 - (u - x) : x - (u - 1.0), u);
+    hu = hu0 & 0x000fffff;
+    const bool up = hu >= 0x6a09e;
+    const uint64_t lo = as_u64(u) & 0xffffffffull;
+    f = as_double(((uint64_t)(uint32_t)(hu | (up ? 0x3fe00000 : 0x3ff00000)) << 32) | lo) - 1.0;
+    k = up ? k + 1 : k;
+    hu = up ? (0x00100000 - hu) >> 2 : hu;
+  }
   const double hfsq = 0.5 * f * f;
-  const double s = f / (2.0 + f);
+  const double s = div_rn(f, 2.0 + f);
   const double z = s * s;
   const double R1 = z * Lp1, z2 = z * z;
   const double R2 = Lp2 + z * Lp3, z4 = z2 * z2;
   const double R3 = Lp4 + z * Lp5, z6 = z4 * z2;
   const double R4 = Lp6 + z * Lp7;
   const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
-  double r = k == 0 ? f - (hfsq - s * (hfsq + R))
-                    : k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+  double r;
+  if (k == 0) r = f - (hfsq - s * (hfsq + R));
+  else r = k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
   if (hu == 0) {  // |f| < 2^-20 (x = 1 here)
     if (f == 0.0) {
       r = k == 0 ? 0.0 : k * ln2_hi + (c + k * ln2_lo);

@@ -142,7 +142,7 @@ def device_count() -> int:
 
 
 REFMATH_FNS = {"log": 0, "exp": 1, "expit": 2, "logaddexp": 3, "glibc_exp": 4, "glibc_log1p": 5,
-               "sqrt": 6, "div": 7}
+               "sqrt": 6, "div": 7, "log1p_unit": 8}
 
 
 def refmath_probe(fn: str, x, y=None) -> np.ndarray:

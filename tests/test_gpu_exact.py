@@ -44,6 +44,16 @@ def test_refmath_on_the_device_equals_numpy_scipy_glibc():
     assert _bits_equal(_lib.refmath_probe("glibc_exp", x), [math.exp(v) for v in x])
     x = np.exp(rng.uniform(np.log(1e-300), 0, 1 << 16))
     assert _bits_equal(_lib.refmath_probe("glibc_log1p", x), [math.log1p(v) for v in x])
+    # logaddexp's log1p on [0, 1] (its normalising branch from 0.41422, the
+    # divisions without scaling): dense near the branch points and the ends
+    x = np.concatenate([rng.uniform(0, 1, 1 << 17), rng.uniform(0.41, 0.42, 1 << 15),
+                        np.exp(rng.uniform(np.log(1e-320), 0, 1 << 15)), 1.0 - rng.uniform(0, 1e-6, 1 << 14),
+                        [0.0, 1.0, 0.41421356, 2.0 ** -29, 2.0 ** -54, 5e-324]])
+    assert _bits_equal(_lib.refmath_probe("log1p_unit", x), [math.log1p(v) for v in x])
+    a = rng.normal(-60, 25, n)
+    b = a + rng.normal(0, 1.0, n)     # |a - b| < 0.88 for most: the normalising branch
+    b[::5] = a[::5] + rng.normal(0, 1e-9, len(b[::5]))
+    assert _bits_equal(_lib.refmath_probe("logaddexp", a, b), np.logaddexp(a, b))
     # the IEEE operations the optimiser's control needs correctly rounded
     x = np.exp(rng.uniform(-700, 700, n))
     assert _bits_equal(_lib.refmath_probe("sqrt", x), np.sqrt(x))
