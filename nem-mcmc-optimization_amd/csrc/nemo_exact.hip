@@ -112,25 +112,61 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
   const int lane = t & (kWave - 1);
   const double* urow = U + (size_t)i * E;
   double* crow = cells + ((size_t)b * (S + 1) + i) * E;
-  constexpr int kU = 8;  // parents per batch of loads ahead of their adds
-  for (int word = __builtin_amdgcn_readfirstlane(t / kWave); word * kWave < E; word += kCellsThreads / kWave) {
+  const double2* v2 = reinterpret_cast<const double2*>(&v[0][0]);
+  const int nwaves = __builtin_amdgcn_readfirstlane(blockDim.x / kWave);
+  // a wave takes kGW consecutive words at a time: per parent one index, one
+  // scalar load of the kGW words and one broadcast read of the two factors
+  // serve kGW cells per lane
+  constexpr int kGW = 4, kU = 4;
+  const int ngroups = nwords / kGW;
+  int g = __builtin_amdgcn_readfirstlane(t / kWave);
+  for (; g < ngroups; g += nwaves) {
+    double cell[kGW];
+#pragma unroll
+    for (int w = 0; w < kGW; ++w) {
+      const int e = (g * kGW + w) * kWave + lane;
+      cell[w] = e < E ? urow[e] : 0.0;
+    }
+    const uint64_t* dw = d1w + g * kGW;
+    int q = 0;
+    for (; q + kU <= pi; q += kU) {
+      uint64_t wd[kU][kGW];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords;
+#pragma unroll
+        for (int w = 0; w < kGW; ++w) wd[u][w] = p[w];
+      }
+      double2 f[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) f[u] = v2[q + u];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+#pragma unroll
+        for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(wd[u][w]) ? f[u].y : f[u].x);
+      }
+    }
+    for (; q < pi; ++q) {
+      const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords;
+      const double2 f = v2[q];
+#pragma unroll
+      for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(p[w]) ? f.y : f.x);
+    }
+#pragma unroll
+    for (int w = 0; w < kGW; ++w) {
+      const int e = (g * kGW + w) * kWave + lane;
+      if (e < E) crow[e] = cell[w];
+    }
+  }
+  // the words past the last whole group, one at a time
+  for (int word = ngroups * kGW + (g - ngroups); word < nwords; word += nwaves) {
     const int e = word * kWave + lane;
     double cell = e < E ? urow[e] : 0.0;
     const uint64_t* dw = d1w + word;
-    int q = 0;
-    for (; q + kU <= pi; q += kU) {
-      uint64_t wd[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) wd[u] = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords];
-      double f[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) f[u] = v[q + u][__builtin_amdgcn_inverse_ballot_w64(wd[u]) ? 1 : 0];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) cell = cell + f[u];
-    }
-    for (; q < pi; ++q) {
+    for (int q = 0; q < pi; ++q) {
       const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords];
-      cell = cell + v[q][__builtin_amdgcn_inverse_ballot_w64(wd) ? 1 : 0];
+      const double2 f = v2[q];
+      cell = cell + (__builtin_amdgcn_inverse_ballot_w64(wd) ? f.y : f.x);
     }
     if (e < E) crow[e] = cell;
   }
@@ -738,7 +774,9 @@ size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjecti
 hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
   const int S = c.S, E = c.E;
-  exact_cells_kernel<<<dim3(batch * (S + 1)), kCellsThreads, 0, st>>>(S, E, d_pos, d_w01, c.d_xlo, c.d_xhi, c.d_D1w,
+  // one wave per group of 4 D1 words, at most kCellsThreads / 64 waves
+  const int cw = std::min(kCellsThreads / kWave, std::max(1, (c.nwords + 3) / 4));
+  exact_cells_kernel<<<dim3(batch * (S + 1)), cw * kWave, 0, st>>>(S, E, d_pos, d_w01, c.d_xlo, c.d_xhi, c.d_D1w,
                                                                       c.nwords, c.d_U64, d_cells);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
