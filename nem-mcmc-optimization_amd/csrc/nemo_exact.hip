@@ -70,18 +70,21 @@ __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nword
 }
 
 // ---------------------------------------------------------------------------
-// cells: one block per (evaluation, child i).  The block first evaluates the
-// child's two log factors per parent, log((1 - s) + s x) for x = exp(lo_j),
-// exp(hi_j) (numpy: `1.0 - expit(w) + expit(w) * np.exp(T)`, then np.log),
-// then each thread adds them to U[i][e] in pi's parent order.  Row S
-// (attached to nothing) is U[S].  Cells go to `cells` [b][S+1][E].
-// A wave covers the 64 effects of one D1 word at a time, so a parent's word
-// is one scalar load and its bits are the wave's lane mask (inverse ballot)
-// choosing between the parent's two factors.
+// cells: one block per (evaluation, `rows` consecutive children i).  The block
+// first evaluates each child's two log factors per parent, log((1 - s) + s x)
+// for x = exp(lo_j), exp(hi_j) (numpy: `1.0 - expit(w) + expit(w) *
+// np.exp(T)`, then np.log), then each thread adds them to U[i][e] in pi's
+// parent order.  Row S (attached to nothing) is U[S].  Cells go to `cells`
+// [b][S+1][E].  A wave takes kGW consecutive D1 words at a time: per parent
+// one scalar load of the words (their bits are the wave's lane masks, inverse
+// ballot) and one broadcast read of the factor pair serve kGW cells per lane.
+// Several children per block share the block's table fill and permutation
+// (large batches); one child per block keeps small batches wide.
 // ---------------------------------------------------------------------------
-constexpr int kCellsThreads = 512;
+constexpr int kCellsThreads = 512, kCellsRows = 8, kCellsSlots = 512;
 
-__global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E, const int32_t* __restrict__ pos,
+__global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E, int rows,
+                                                                    const int32_t* __restrict__ pos,
                                                                     const double* __restrict__ w01,
                                                                     const double* __restrict__ xlo,
                                                                     const double* __restrict__ xhi,
@@ -91,84 +94,90 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ int perm[kMaxS];
-  __shared__ double v[kMaxS][2];
-  const int i = blockIdx.x % (S + 1);
-  const int b = blockIdx.x / (S + 1);
+  __shared__ double v[kCellsSlots][2];   // [rows][S] factor pairs, rows * S <= kCellsSlots
+  const int nchunk = (S + rows) / rows;   // ceil((S + 1) / rows)
+  const int i0 = (blockIdx.x % nchunk) * rows;
+  const int b = blockIdx.x / nchunk;
+  const int nr = min(rows, S + 1 - i0);
   const int t = threadIdx.x;
   const int32_t* pb = pos + (size_t)b * S;
-  const int pi = i < S ? pb[i] : 0;
-  if (pi > 0) tabs.fill_log(t, blockDim.x);
+  if (i0 < S) tabs.fill_log(t, blockDim.x);
   for (int q = t; q < S; q += blockDim.x) perm[pb[q]] = q;
   __syncthreads();
   const LdsTabs tb = tabs.view();
-  for (int q = t; q < pi; q += blockDim.x) {
-    const int j = perm[q];
-    const double s = w01[((size_t)b * S + i) * S + j];
-    const double oms = 1.0 - s;
-    v[q][0] = refmath::svml_log(oms + s * xlo[j], tb);
-    v[q][1] = refmath::svml_log(oms + s * xhi[j], tb);
+  for (int r = 0; r < nr; ++r) {
+    const int i = i0 + r;
+    const int pi = i < S ? pb[i] : 0;
+    for (int q = t; q < 2 * pi; q += blockDim.x) {   // lo and hi factors on separate lanes
+      const int j = perm[q >> 1];
+      const double s = w01[((size_t)b * S + i) * S + j];
+      v[r * S + (q >> 1)][q & 1] = refmath::svml_log((1.0 - s) + s * ((q & 1) ? xhi[j] : xlo[j]), tb);
+    }
   }
   __syncthreads();
   const int lane = t & (kWave - 1);
-  const double* urow = U + (size_t)i * E;
-  double* crow = cells + ((size_t)b * (S + 1) + i) * E;
-  const double2* v2 = reinterpret_cast<const double2*>(&v[0][0]);
   const int nwaves = __builtin_amdgcn_readfirstlane(blockDim.x / kWave);
-  // a wave takes kGW consecutive words at a time: per parent one index, one
-  // scalar load of the kGW words and one broadcast read of the two factors
-  // serve kGW cells per lane
+  const int w0 = __builtin_amdgcn_readfirstlane(t / kWave);
   constexpr int kGW = 4, kU = 4;
   const int ngroups = nwords / kGW;
-  int g = __builtin_amdgcn_readfirstlane(t / kWave);
-  for (; g < ngroups; g += nwaves) {
-    double cell[kGW];
+  for (int r = 0; r < nr; ++r) {
+    const int i = i0 + r;
+    const int pi = i < S ? pb[i] : 0;
+    const double* urow = U + (size_t)i * E;
+    double* crow = cells + ((size_t)b * (S + 1) + i) * E;
+    const double2* v2 = reinterpret_cast<const double2*>(&v[r * S][0]);
+    int g = w0;
+    for (; g < ngroups; g += nwaves) {
+      double cell[kGW];
 #pragma unroll
-    for (int w = 0; w < kGW; ++w) {
-      const int e = (g * kGW + w) * kWave + lane;
-      cell[w] = e < E ? urow[e] : 0.0;
-    }
-    const uint64_t* dw = d1w + g * kGW;
-    int q = 0;
-    for (; q + kU <= pi; q += kU) {
-      uint64_t wd[kU][kGW];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords;
-#pragma unroll
-        for (int w = 0; w < kGW; ++w) wd[u][w] = p[w];
+      for (int w = 0; w < kGW; ++w) {
+        const int e = (g * kGW + w) * kWave + lane;
+        cell[w] = e < E ? urow[e] : 0.0;
       }
-      double2 f[kU];
+      const uint64_t* dw = d1w + g * kGW;
+      int q = 0;
+      for (; q + kU <= pi; q += kU) {
+        uint64_t wd[kU][kGW];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) f[u] = v2[q + u];
+        for (int u = 0; u < kU; ++u) {
+          const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords;
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
+          for (int w = 0; w < kGW; ++w) wd[u][w] = p[w];
+        }
+        double2 f[kU];
 #pragma unroll
-        for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(wd[u][w]) ? f[u].y : f[u].x);
+        for (int u = 0; u < kU; ++u) f[u] = v2[q + u];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+#pragma unroll
+          for (int w = 0; w < kGW; ++w)
+            cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(wd[u][w]) ? f[u].y : f[u].x);
+        }
+      }
+      for (; q < pi; ++q) {
+        const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords;
+        const double2 f = v2[q];
+#pragma unroll
+        for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(p[w]) ? f.y : f.x);
+      }
+#pragma unroll
+      for (int w = 0; w < kGW; ++w) {
+        const int e = (g * kGW + w) * kWave + lane;
+        if (e < E) crow[e] = cell[w];
       }
     }
-    for (; q < pi; ++q) {
-      const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords;
-      const double2 f = v2[q];
-#pragma unroll
-      for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(p[w]) ? f.y : f.x);
+    // the words past the last whole group, one at a time
+    for (int word = ngroups * kGW + (g - ngroups); word < nwords; word += nwaves) {
+      const int e = word * kWave + lane;
+      double cell = e < E ? urow[e] : 0.0;
+      const uint64_t* dw = d1w + word;
+      for (int q = 0; q < pi; ++q) {
+        const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords];
+        const double2 f = v2[q];
+        cell = cell + (__builtin_amdgcn_inverse_ballot_w64(wd) ? f.y : f.x);
+      }
+      if (e < E) crow[e] = cell;
     }
-#pragma unroll
-    for (int w = 0; w < kGW; ++w) {
-      const int e = (g * kGW + w) * kWave + lane;
-      if (e < E) crow[e] = cell[w];
-    }
-  }
-  // the words past the last whole group, one at a time
-  for (int word = ngroups * kGW + (g - ngroups); word < nwords; word += nwaves) {
-    const int e = word * kWave + lane;
-    double cell = e < E ? urow[e] : 0.0;
-    const uint64_t* dw = d1w + word;
-    for (int q = 0; q < pi; ++q) {
-      const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords];
-      const double2 f = v2[q];
-      cell = cell + (__builtin_amdgcn_inverse_ballot_w64(wd) ? f.y : f.x);
-    }
-    if (e < E) crow[e] = cell;
   }
 }
 
@@ -774,10 +783,13 @@ size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjecti
 hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
   const int S = c.S, E = c.E;
-  // one wave per group of 4 D1 words, at most kCellsThreads / 64 waves
+  // one wave per group of 4 D1 words, at most kCellsThreads / 64 waves; 8
+  // children per block once the batch alone fills the chip
   const int cw = std::min(kCellsThreads / kWave, std::max(1, (c.nwords + 3) / 4));
-  exact_cells_kernel<<<dim3(batch * (S + 1)), cw * kWave, 0, st>>>(S, E, d_pos, d_w01, c.d_xlo, c.d_xhi, c.d_D1w,
-                                                                      c.nwords, c.d_U64, d_cells);
+  const int rows = batch >= 512 ? std::min(kCellsRows, kCellsSlots / S) : 1;
+  const int nchunk = (S + rows) / rows;
+  exact_cells_kernel<<<dim3(batch * nchunk), cw * kWave, 0, st>>>(S, E, rows, d_pos, d_w01, c.d_xlo, c.d_xhi,
+                                                                  c.d_D1w, c.nwords, c.d_U64, d_cells);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   const size_t nthr = (size_t)batch * E;
