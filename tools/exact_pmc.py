@@ -38,6 +38,17 @@ def main():
             out["lds_busy"] = li / (256 * cyc)
             if all("SQ_LDS_BANK_CONFLICT" in d for d in ds):
                 out["lds_conflict_share"] = sum(d["SQ_LDS_BANK_CONFLICT"] for d in ds) / len(ds) / max(li, 1.0)
+        # wave-state split (quad-cycles, summed over waves): parked on a waitcnt /
+        # barrier, stalled at issue, issuing
+        if all("SQ_WAVE_CYCLES" in d for d in ds):
+            wc = sum(d["SQ_WAVE_CYCLES"] for d in ds) / len(ds)
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+                if all(c in d for d in ds):
+                    out[c.lower()[3:] + "_frac"] = sum(d[c] for d in ds) / len(ds) / max(wc, 1.0)
+        if all("TCC_HIT_sum" in d and "TCC_MISS_sum" in d for d in ds):
+            h = sum(d["TCC_HIT_sum"] for d in ds)
+            out["l2_hit_rate"] = h / max(h + sum(d["TCC_MISS_sum"] for d in ds), 1.0)
+            out["l2_req_per_launch"] = (h + sum(d["TCC_MISS_sum"] for d in ds)) / len(ds)
         if all("SQ_WAVES" in d for d in ds):
             out["SQ_WAVES"] = sum(d["SQ_WAVES"] for d in ds) / len(ds)
         print(name, {k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()})

@@ -206,10 +206,12 @@ cut -c1-140 "$P/trace/t_kernel_stats.csv" | head -8
 # (tools/exact_score_probe.py 2048) and the fused step at 1 and 16 chains (tools/step_probe.py)
 task_exact_pmc() (
 P=${PROF_DIR:-gpurun_out/exact_pmc}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
-C="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
-timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$R/$P/score" -o p -- python "$R/tools/exact_score_probe.py" 2048 > "$P/score.log" 2>&1 || exit 1
-python tools/exact_pmc.py "$P/score/p_counter_collection.csv"
-for n in 1 16; do
+C=${COUNTERS:-"SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"}
+if [ -z "$NO_SCORE" ]; then
+  timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$R/$P/score" -o p -- python "$R/tools/exact_score_probe.py" 2048 > "$P/score.log" 2>&1 || exit 1
+  python tools/exact_pmc.py "$P/score/p_counter_collection.csv"
+fi
+for n in ${CHAINS:-1 16}; do
   timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$R/$P/step$n" -o p -- python "$R/tools/step_probe.py" $n > "$P/step$n.log" 2>&1 || exit 1
   echo "== step n=$n"; python tools/exact_pmc.py "$P/step$n/p_counter_collection.csv"
 done
