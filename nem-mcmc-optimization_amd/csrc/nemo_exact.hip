@@ -256,8 +256,17 @@ __device__ __forceinline__ double wave_seq_sum(const double* __restrict__ cs, in
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int n = E - base < kWave ? E - base : kWave;
     if (n == kWave) {
+      // 32 values read before their 32 adds: the chain waits on one read latency
+      // per half row, not on one per pair of adds
 #pragma unroll
-      for (int l = 0; l < kWave; ++l) acc = acc + row[l];
+      for (int h = 0; h < kWave; h += 32) {
+        double vals[32];
+#pragma unroll
+        for (int l = 0; l < 32; ++l) vals[l] = row[h + l];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int l = 0; l < 32; ++l) acc = acc + vals[l];
+      }
     } else {
       for (int l = 0; l < n; ++l) acc = acc + row[l];
     }
