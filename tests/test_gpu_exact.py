@@ -146,6 +146,21 @@ def test_exact_score_dev_equals_reference_goldens():
     w01 = expit(rng.uniform(-6, 6, (300, s, s)))
     ll, _, _ = run(pos, w01, False)
     assert _bits_equal(ll, eng.score(pos, w01))
+    # the cells alone (d_cells), against the host-pointer exact path's cells
+    b = 5
+    dpos = torch.from_numpy(pos[:b]).cuda()
+    dw = torch.from_numpy(w01[:b]).cuda()
+    dll = torch.zeros(b, dtype=torch.float64, device="cuda")
+    dcells = torch.zeros((b, s + 1, e), dtype=torch.float64, device="cuda")
+    _lib.check(lib.nemo_score_dev(eng._ctx, b, dpos.data_ptr(), dw.data_ptr(), 0, dll.data_ptr(), None,
+                                  dcells.data_ptr(), None, st))
+    torch.cuda.synchronize()
+    host = eng.score(pos[:b], w01[:b], want_cells=True)
+    assert _bits_equal(dcells.cpu().numpy(), host["cells"]) and _bits_equal(dll.cpu().numpy(), host["ll"])
+    # cells and order weights share the exact path's one buffer: refused
+    with pytest.raises(RuntimeError):
+        _lib.check(lib.nemo_score_dev(eng._ctx, b, dpos.data_ptr(), dw.data_ptr(), 0, dll.data_ptr(), None,
+                                      dcells.data_ptr(), dcells.data_ptr(), st))
     eng.set_option("exact_dev", 0)   # the fast kernels again: within 1e-6, not the same bits
     ll_fast, _, _ = run(pos, w01, False)
     assert np.max(np.abs(ll_fast - ll)) <= 1e-6
