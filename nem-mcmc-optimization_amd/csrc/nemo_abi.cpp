@@ -147,7 +147,8 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_D1w,  c.d_elo,  c.d_ehi,  c.d_U64,  c.d_fDp,  c.d_fG,  c.d_fperm,
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
-                  c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf};
+                  c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf,
+                  c.d_xa,   c.d_xbits, c.d_pwpos};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -200,11 +201,6 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_wdag, nc * S * S));
     HIPCHK(dalloc(&c.d_info, nc * S * S));
     HIPCHK(dalloc(&c.d_xcs, 2 * nc * E));
-    HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
-    if (nemo::exact_supported(c)) {   // the exact local optima's c rows (nemo_exact.hip)
-      c.cap_xcbuf = (size_t)nc * nemo::pairs_per_chain(c.S, 0) * nemo::exact_cbuf_doubles(c);
-      HIPCHK(dalloc(&c.d_xcbuf, c.cap_xcbuf));
-    }
     c.cap_chains = nc;
   }
   return NEMO_OK;
@@ -320,24 +316,37 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     // and the wave layout of numpy's pairwise sum of E terms
     c.exact_ok = false;
     nemo::host::PairwisePlan pl;
-    if (nemo::host::build_pairwise_plan(c.E, pl) && pl.ns <= 4 && pl.nh <= 8) {
+    if (nemo::host::build_pairwise_plan(c.E, pl) && pl.ns <= nemo::kExactMaxSlots && pl.nh <= 8) {
       std::vector<double> xlo(S), xhi(S);
       for (size_t j = 0; j < S; ++j) {
         xlo[j] = nemo::refmath::svml_exp(tlo[j]);
         xhi[j] = nemo::refmath::svml_exp(thi[j]);
       }
+      // the partner rows padded to the 8 heights the kernels read (-1: none)
+      std::vector<int32_t> partner = pl.partner;
+      partner.resize((size_t)8 * 64, -1);
       std::vector<int32_t> dev;
       dev.insert(dev.end(), pl.start.begin(), pl.start.end());
       dev.insert(dev.end(), pl.cnt.begin(), pl.cnt.end());
       dev.insert(dev.end(), pl.rem.begin(), pl.rem.end());
       dev.insert(dev.end(), pl.nrem.begin(), pl.nrem.end());
-      dev.insert(dev.end(), pl.partner.begin(), pl.partner.end());
+      dev.insert(dev.end(), partner.begin(), partner.end());
+      // the recompute form's element -> plan position map and lv bits per
+      // (parent row, slot, lane)
+      std::vector<int32_t> ppos;
+      std::vector<uint32_t> bits;
+      nemo::host::plan_positions(pl, ppos);
+      nemo::host::plan_lv_bits(pl, c.S, d1.data(), nwords, bits);
       HIPCHK(dalloc(&c.d_xlo, S));
       HIPCHK(dalloc(&c.d_xhi, S));
       HIPCHK(dalloc(&c.d_pwplan, dev.size()));
+      HIPCHK(dalloc(&c.d_pwpos, ppos.size()));
+      HIPCHK(dalloc(&c.d_xbits, bits.size()));
       HIPCHK(hipMemcpy(c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(c.d_pwplan, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(c.d_pwpos, ppos.data(), ppos.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(c.d_xbits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
       c.pw_ns = pl.ns;
       c.pw_nh = pl.nh;
       c.pw_maxrem = pl.maxrem;
@@ -349,12 +358,6 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     const int nb = c.cap_batch;
     c.cap_batch = 0;
     int rc2 = nemo_reserve(ctx, nb, 0);
-    if (rc2) return rc2;
-  }
-  if (c.cap_chains > 0 && nemo::exact_supported(c) && !c.d_xcbuf) {   // chains reserved before staging
-    const int nc = c.cap_chains;
-    c.cap_chains = 0;
-    int rc2 = nemo_reserve(ctx, 0, nc);
     if (rc2) return rc2;
   }
   c.staged = true;
@@ -481,8 +484,13 @@ static bool use_factored(const Ctx& c) {
 // ---------------------------------------------------------------------------
 // A4+A5
 // ---------------------------------------------------------------------------
-int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double* d_w01, int cap,
-                   double* d_ll, double* d_cs, double* d_cells, double* d_ow, void* stream) {
+}  // extern "C"
+
+// nemo_score_dev; allow_exact: the option exact_dev may route the call to the
+// exact kernels (nemo_score's own fall-through passes false: it takes the
+// exact path itself when option exact asks for it)
+static int score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double* d_w01, int cap, double* d_ll,
+                     double* d_cs, double* d_cells, double* d_ow, void* stream, bool allow_exact) {
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
   Ctx& c = ctx->c;
@@ -493,14 +501,14 @@ int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double*
   hipStream_t st = pick(ctx, stream);
   if (c.score_path == 2 && !c.factored)
     return fail(NEMO_ERR_STATE, "score_path=2 (factored) but the staged table is not factorable");
-  if (ctx->exact_dev && use_factored(c) && c.fact_kernel == 0 && (cap == 0 || cap >= (int)c.S - 1) &&
-      nemo::exact_supported(c)) {
+  if (allow_exact && ctx->exact_dev && use_factored(c) && c.fact_kernel == 0 && nemo::exact_supported(c)) {
     // nemo_score's exact path on device buffers: the cells are built in the
     // caller's d_ow (turned into order weights in place) or d_cells, else in
     // the context's scratch
     if (d_cells && d_ow) return fail(NEMO_ERR_ARG, "exact_dev: cells and order weights share one buffer");
     double* cells = d_ow ? d_ow : d_cells ? d_cells : c.d_ow;
-    HIPCHK(nemo::launch_exact_eval(c, batch, d_pos, d_w01, cells, d_cs ? d_cs : c.d_cs, d_ll, d_ow != nullptr, st));
+    HIPCHK(nemo::launch_exact_eval(c, batch, cap, d_pos, d_w01, cells, d_cs ? d_cs : c.d_cs, d_ll, d_ow != nullptr,
+                                   st));
     if (cells == c.d_ow) c.ow_chains = 0;  // d_ow no longer holds fused-step order weights
     return NEMO_OK;
   }
@@ -511,6 +519,13 @@ int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double*
   HIPCHK(nemo::launch_prep(c, batch, cap, d_pos, d_w01, c.d_rows, c.d_sw, c.d_cnt, nullptr, st));
   HIPCHK(nemo::launch_score(c, batch, c.d_rows, c.d_sw, c.d_cnt, d_ll, d_cs, d_cells, d_ow, st));
   return NEMO_OK;
+}
+
+extern "C" {
+
+int nemo_score_dev(nemo_ctx* ctx, int batch, const int32_t* d_pos, const double* d_w01, int cap,
+                   double* d_ll, double* d_cs, double* d_cells, double* d_ow, void* stream) {
+  return score_dev(ctx, batch, d_pos, d_w01, cap, d_ll, d_cs, d_cells, d_ow, stream, true);
 }
 
 int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, int cap,
@@ -525,15 +540,15 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if ((rc = nemo_reserve(ctx, batch, 0))) return rc;
   const size_t S = c.S, E = c.E;
   hipStream_t st = c.stream;
-  if (!(cells_out && ow_out) && use_factored(c) && c.exact && c.fact_kernel == 0 &&
-      (cap == 0 || cap >= (int)S - 1) && nemo::exact_supported(c)) {
+  if (use_factored(c) && c.exact && c.fact_kernel == 0 && nemo::exact_supported(c)) {
     // the reference's arithmetic (nemo_exact.hip) whatever the batch, so a
     // score never depends on how many orders share the call: ll and, when
-    // asked, the column sums cs and the order weights (calculate_ll's ow) or
-    // the cells (the order weights are written over the cells, so not both);
-    // pos and W in one copy.  An explicitly chosen kernel (option
-    // fact_kernel) runs as chosen; the batched device entry (nemo_score_dev)
-    // keeps the fixed-point kernels.
+    // asked, the column sums cs, the cells and the order weights
+    // (calculate_ll's ow; written over the cells, so a call that wants both
+    // gets the cells from a first pass); pos and W in one copy.  An
+    // explicitly chosen kernel (option fact_kernel) runs as chosen; the
+    // batched device entry (nemo_score_dev) keeps the fixed-point kernels
+    // unless option exact_dev is set.
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t n = batch, o_w01 = up(n * S * 4), o_ll = o_w01 + up(n * S * S * 8), total = o_ll + up(n * 8);
     if ((rc = step_stage(c, 0, total))) return rc;
@@ -542,7 +557,12 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
     memcpy(hs, pos, n * S * 4);
     memcpy(hs + o_w01, w01, n * S * S * 8);
     HIPCHK(hipMemcpyAsync(ds, hs, o_ll, hipMemcpyHostToDevice, st));
-    HIPCHK(nemo::launch_exact_eval(c, batch, (const int32_t*)ds, (const double*)(ds + o_w01), c.d_ow, c.d_cs,
+    if (cells_out && ow_out) {   // the cells first, then the pass below writes the order weights over them
+      HIPCHK(nemo::launch_exact_eval(c, batch, cap, (const int32_t*)ds, (const double*)(ds + o_w01), c.d_ow,
+                                     c.d_cs, nullptr, false, st));
+      HIPCHK(hipMemcpyAsync(cells_out, c.d_ow, n * (S + 1) * E * 8, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(nemo::launch_exact_eval(c, batch, cap, (const int32_t*)ds, (const double*)(ds + o_w01), c.d_ow, c.d_cs,
                                    (double*)(ds + o_ll), ow_out != nullptr, st));
     HIPCHK(hipMemcpyAsync(hs + o_ll, ds + o_ll, n * 8, hipMemcpyDeviceToHost, st));
     if (cs_out) HIPCHK(hipMemcpyAsync(cs_out, c.d_cs, n * E * 8, hipMemcpyDeviceToHost, st));
@@ -590,8 +610,8 @@ int nemo_score(nemo_ctx* ctx, int batch, const int32_t* pos, const double* w01, 
   if (cells_out) HIPCHK(hipMallocAsync((void**)&d_cells, batch * (S + 1) * E * 8, st));
   HIPCHK(hipMemcpyAsync(c.d_pos, pos, batch * S * 4, hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync(c.d_w01, w01, batch * S * S * 8, hipMemcpyHostToDevice, st));
-  rc = nemo_score_dev(ctx, batch, c.d_pos, c.d_w01, cap, c.d_ll, cs_out ? c.d_cs : nullptr,
-                      d_cells, ow_out ? c.d_ow : nullptr, st);
+  rc = score_dev(ctx, batch, c.d_pos, c.d_w01, cap, c.d_ll, cs_out ? c.d_cs : nullptr, d_cells,
+                 ow_out ? c.d_ow : nullptr, st, false);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(ll_out, c.d_ll, batch * 8, hipMemcpyDeviceToHost, st));
   if (cs_out) HIPCHK(hipMemcpyAsync(cs_out, c.d_cs, batch * E * 8, hipMemcpyDeviceToHost, st));
@@ -667,7 +687,8 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, 
     return fail(NEMO_ERR_ARG, "n=%d / null pointer", n);
   if (n == 0) return NEMO_OK;
   Ctx& c = ctx->c;
-  if (c.E > 80 * 64) return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by local_opt", c.E);
+  if (!(c.exact && nemo::exact_supported(c)) && c.E > 80 * 64)
+    return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by the fast local optima (option exact 0)", c.E);
   const size_t E = c.E;
   hipStream_t st = c.stream;
   double *d_c = nullptr, *d_a = nullptr, *d_x = nullptr, *d_o = nullptr;
@@ -712,6 +733,47 @@ int nemo_local_opt(nemo_ctx* ctx, int n, const double* cvec, const double* anc, 
 
 namespace {
 
+// the fused step takes the reference's arithmetic for this call (option
+// exact and a factored model the exact kernels cover; any parent cap)
+bool step_exact(const Ctx& c, int) { return use_factored(c) && c.exact && nemo::exact_supported(c); }
+
+// the exact fused step's buffers for nchains chains, allocated on first use
+// (never captured: step_start and nemo_optimal_weights_dev call this before
+// any launch): eval #2's cells and either the recompute form's a rows
+// (d_xa, chains x S x plan: 1.1 MB per chain at C3) or the stored form's c
+// rows (d_xcbuf, chains x pairs x plan: 35 MB per chain at C3).  A failed
+// allocation is the call's error -- the step never drops to other arithmetic
+int exact_reserve(Ctx& c, int nchains) {
+  const size_t S = c.S, E = c.E, plan = nemo::exact_plan_doubles(c), nc = (size_t)std::max(nchains, 1);
+  if (!c.d_xcells2 || c.cap_xcells2 < nc) {
+    ++c.graph_epoch;
+    HIPCHK(hipStreamSynchronize(c.stream));
+    HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
+    c.cap_xcells2 = nc;
+  }
+  if (c.exact_cform == 1) {
+    const size_t need = nc * S * plan;
+    if (need > c.cap_xa) {
+      ++c.graph_epoch;
+      HIPCHK(hipStreamSynchronize(c.stream));
+      HIPCHK(dalloc(&c.d_xa, need));
+      // positions without an element stay 0 (the order-weight launch writes
+      // only real elements): their c is 0 / b = 0, as in a stored row
+      HIPCHK(hipMemset(c.d_xa, 0, need * 8));
+      c.cap_xa = need;
+    }
+  } else {
+    const size_t need = nc * (size_t)nemo::pairs_per_chain(c.S, 0) * plan;
+    if (need > c.cap_xcbuf) {
+      ++c.graph_epoch;
+      HIPCHK(hipStreamSynchronize(c.stream));
+      HIPCHK(dalloc(&c.d_xcbuf, need));
+      c.cap_xcbuf = need;
+    }
+  }
+  return NEMO_OK;
+}
+
 // the fused step's device work on `stream`.  d_part2 null: eval #2's ll is
 // summed on the device into d_ll_dag.  Set (the staged host path): eval #2's
 // per-evaluation partials go to d_part2 (stride *np2) and are left for the
@@ -729,25 +791,32 @@ int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, co
   if (nchains == 0) return NEMO_OK;
   if (nchains > c.cap_chains || nchains > c.cap_batch)
     return fail(NEMO_ERR_STATE, "nchains %d > reserved %d", nchains, c.cap_chains);
-  if (c.E > 80 * 64) return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by local_opt", c.E);
+  if (!step_exact(c, cap) && c.E > 80 * 64)
+    return fail(NEMO_ERR_ARG, "E=%d > 5120 not supported by the fast local optima (option exact 0)", c.E);
   if (!d_pos || !d_w01 || !d_anc || !d_w_new || !d_ll1 || !d_ll_dag)
     return fail(NEMO_ERR_ARG, "null device pointer");
   hipStream_t st = pick(ctx, stream);
-  const int npairs = nemo::pairs_per_chain(c.S, cap);
-  if (use_factored(c) && c.exact && cap == 0 && nemo::exact_supported(c)) {
+  if (step_exact(c, cap)) {
     // the reference's own arithmetic (nemo_exact.hip): eval #1's cells and
-    // order weights in d_ow, the local optima (eval #1's ll summed by the
-    // launch's appended blocks), eval #2 summed on the device
+    // order weights in d_ow (and the local optima's a rows), the local optima
+    // (eval #1's ll summed by the launch's appended blocks), eval #2 summed on
+    // the device.  With a cap, the capped parent lists throughout (the prep's
+    // pair lists, both evaluations' cells)
+    if (c.cap_xcells2 < (size_t)nchains || (c.exact_cform == 1 ? !c.d_xa : !c.d_xcbuf))
+      return fail(NEMO_ERR_STATE, "exact step buffers not reserved for %d chains", nchains);
     double* cs1 = c.d_xcs;
     double* cs2 = c.d_xcs + (size_t)nchains * c.E;
     HIPCHK(nemo::launch_step_prep(c, nchains, cap, d_pos, d_w01, d_info, st));
-    HIPCHK(nemo::launch_exact_eval(c, nchains, d_pos, d_w01, c.d_ow, cs1, nullptr, true, st));
-    HIPCHK(nemo::launch_local_opt_exact(c, nchains, npairs, c.d_pairs, d_w01, d_anc, c.d_ow, sig0, sig1, d_w_new,
+    HIPCHK(nemo::launch_exact_eval(c, nchains, cap, d_pos, d_w01, c.d_ow, cs1, nullptr, true, st,
+                                   c.exact_cform == 1 ? c.d_xa : nullptr));
+    HIPCHK(nemo::launch_local_opt_exact(c, nchains, nemo::pairs_per_chain(c.S, cap), c.d_pairs, d_w01, d_anc, c.d_ow,
+                                        sig0, sig1, d_w_new,
                                         c.d_wdag, d_info, cs1, d_ll1, st));
-    HIPCHK(nemo::launch_exact_eval(c, nchains, d_pos, c.d_wdag, c.d_xcells2, cs2, d_ll_dag, false, st));
+    HIPCHK(nemo::launch_exact_eval(c, nchains, cap, d_pos, c.d_wdag, c.d_xcells2, cs2, d_ll_dag, false, st));
     c.ow_chains = nchains;
     return NEMO_OK;
   }
+  const int npairs = nemo::pairs_per_chain(c.S, cap);
   // eval #1 with order weights (nem_order_mcmc.py:181-182).  Factored: one
   // prep launch for the pair lists (info rows preset to -1) and eval #1's
   // Delta, and eval #1's partial sums ride in the local-optimum launch -- two
@@ -791,6 +860,11 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
                              const double* d_anc, double sig0, double sig1, int cap,
                              double* d_w_new, double* d_ll1, double* d_ll_dag, int32_t* d_info,
                              void* stream) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (nchains > 0 && nchains <= ctx->c.cap_chains && cap >= 0 && step_exact(ctx->c, cap) &&
+      (rc = exact_reserve(ctx->c, nchains)))
+    return rc;
   return optimal_weights_enqueue(ctx, nchains, d_pos, d_w01, d_anc, sig0, sig1, cap, d_w_new, d_ll1, d_ll_dag,
                                  d_info, stream, nullptr, nullptr);
 }
@@ -840,6 +914,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   Ctx& c = ctx->c;
   if ((rc = check_pos(pos, nchains, c.S))) return rc;
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
+  if (cap >= 0 && step_exact(c, cap) && (rc = exact_reserve(c, nchains))) return rc;
   const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
   const StepLayout L(S, n, step_npart(c));
@@ -1194,6 +1269,15 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.exact_form = value;
     return NEMO_OK;
   }
+  if (strcmp(name, "exact_cform") == 0) {
+    if (value < 0 || value > 1) return fail(NEMO_ERR_ARG, "exact_cform %d (0 stored, 1 recomputed)", value);
+    ctx->c.exact_cform = value;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "exact_xcd") == 0) {
+    ctx->c.exact_xcd = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "exact_lat_waves") == 0) {
     if (value < 0) return fail(NEMO_ERR_ARG, "exact_lat_waves %d", value);
     ctx->c.exact_lat_waves = value;
@@ -1262,6 +1346,8 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact") == 0) *value = c.exact;
   else if (strcmp(name, "exact_dev") == 0) *value = ctx->exact_dev;
   else if (strcmp(name, "exact_form") == 0) *value = c.exact_form;
+  else if (strcmp(name, "exact_cform") == 0) *value = c.exact_cform;
+  else if (strcmp(name, "exact_xcd") == 0) *value = c.exact_xcd;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;

@@ -69,6 +69,17 @@ __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nword
   return (int)((d1w[(size_t)j * nwords + (e >> 6)] >> (e & 63)) & 1ull);
 }
 
+// XCD-contiguous block order (blocks are dealt round-robin to the 8 XCDs, so
+// physical block P runs on XCD P % 8): XCD x takes the x-th contiguous range of
+// the n logical blocks, so the optima in flight on one XCD share few chains
+// and their parents' a rows stay in that XCD's L2.  Bijective on [0, n);
+// blocks >= n (appended work) keep their index.
+__device__ __forceinline__ int xcd_block(int on, int P, int n) {
+  if (!on || P >= n) return P;
+  const int x = P & 7, k = P >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + k;
+}
+
 // ---------------------------------------------------------------------------
 // cells: one block per (evaluation, `rows` consecutive children i).  The block
 // first evaluates each child's two log factors per parent, log((1 - s) + s x)
@@ -83,7 +94,7 @@ __device__ __forceinline__ int d1bit(const uint64_t* __restrict__ d1w, int nword
 // ---------------------------------------------------------------------------
 constexpr int kCellsThreads = 512, kCellsRows = 8, kCellsSlots = 512;
 
-__global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E, int rows,
+__global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E, int rows, int cap,
                                                                     const int32_t* __restrict__ pos,
                                                                     const double* __restrict__ w01,
                                                                     const double* __restrict__ xlo,
@@ -108,8 +119,9 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
   for (int r = 0; r < nr; ++r) {
     const int i = i0 + r;
     const int pi = i < S ? pb[i] : 0;
-    for (int q = t; q < 2 * pi; q += blockDim.x) {   // lo and hi factors on separate lanes
-      const int j = perm[q >> 1];
+    const int lo = (cap > 0 && pi > cap) ? pi - cap : 0;   // with a cap: the last `cap` parents
+    for (int q = t; q < 2 * (pi - lo); q += blockDim.x) {   // lo and hi factors on separate lanes
+      const int j = perm[lo + (q >> 1)];
       const double s = w01[((size_t)b * S + i) * S + j];
       v[r * S + (q >> 1)][q & 1] = refmath::svml_log((1.0 - s) + s * ((q & 1) ? xhi[j] : xlo[j]), tb);
     }
@@ -122,7 +134,10 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
   const int ngroups = nwords / kGW;
   for (int r = 0; r < nr; ++r) {
     const int i = i0 + r;
-    const int pi = i < S ? pb[i] : 0;
+    const int p0 = i < S ? pb[i] : 0;
+    const int lo = (cap > 0 && p0 > cap) ? p0 - cap : 0;
+    const int pi = p0 - lo;       // the parents perm[lo ..], in pi's order
+    const int* pp = perm + lo;
     const double* urow = U + (size_t)i * E;
     double* crow = cells + ((size_t)b * (S + 1) + i) * E;
     const double2* v2 = reinterpret_cast<const double2*>(&v[r * S][0]);
@@ -140,7 +155,7 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
         uint64_t wd[kU][kGW];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-          const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q + u]) * nwords;
+          const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(pp[q + u]) * nwords;
 #pragma unroll
           for (int w = 0; w < kGW; ++w) wd[u][w] = p[w];
         }
@@ -155,7 +170,7 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
         }
       }
       for (; q < pi; ++q) {
-        const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords;
+        const uint64_t* p = dw + (size_t)__builtin_amdgcn_readfirstlane(pp[q]) * nwords;
         const double2 f = v2[q];
 #pragma unroll
         for (int w = 0; w < kGW; ++w) cell[w] = cell[w] + (__builtin_amdgcn_inverse_ballot_w64(p[w]) ? f.y : f.x);
@@ -172,7 +187,7 @@ __global__ __launch_bounds__(kCellsThreads) void exact_cells_kernel(int S, int E
       double cell = e < E ? urow[e] : 0.0;
       const uint64_t* dw = d1w + word;
       for (int q = 0; q < pi; ++q) {
-        const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(perm[q]) * nwords];
+        const uint64_t wd = dw[(size_t)__builtin_amdgcn_readfirstlane(pp[q]) * nwords];
         const double2 f = v2[q];
         cell = cell + (__builtin_amdgcn_inverse_ballot_w64(wd) ? f.y : f.x);
       }
@@ -224,9 +239,14 @@ __global__ __launch_bounds__(256) void exact_fold_kernel(int S, int E, int batch
 }
 
 // order weights in place: cell = exp(cell - cs) (nem_order_mcmc.py:92), one
-// thread per cell
+// thread per cell.  With xa (the fused step's recompute form): also the local
+// optima's a = (lv - 1) * ow (nem_order_mcmc.py:161-162, lv = np.exp(T[i][k])
+// of parent row k) at the element's plan position, [batch][S][plan]
 __global__ __launch_bounds__(256) void exact_ow_kernel(int S, int E, int batch, double* __restrict__ cells,
-                                                       const double* __restrict__ cs) {
+                                                       const double* __restrict__ cs, double* __restrict__ xa,
+                                                       const int32_t* __restrict__ pwpos, int plan_doubles,
+                                                       const double* __restrict__ xlo, const double* __restrict__ xhi,
+                                                       const uint64_t* __restrict__ d1w, int nwords) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   tabs.fill_exp(threadIdx.x, blockDim.x);
@@ -235,8 +255,15 @@ __global__ __launch_bounds__(256) void exact_ow_kernel(int S, int E, int batch, 
   const size_t n = (size_t)batch * (S + 1) * E;
   if (g >= n) return;
   const int e = (int)(g % E);
-  const size_t b = g / ((size_t)(S + 1) * E);
-  cells[g] = refmath::svml_exp(cells[g] - cs[b * E + e], tabs.view());
+  const size_t rb = g / E;   // b * (S + 1) + row
+  const size_t b = rb / (S + 1);
+  const int row = (int)(rb - b * (S + 1));
+  const double ow = refmath::svml_exp(cells[g] - cs[b * E + e], tabs.view());
+  cells[g] = ow;
+  if (xa && row < S) {
+    const double lv = d1bit(d1w, nwords, row, e) ? xhi[row] : xlo[row];
+    xa[(b * S + row) * (size_t)plan_doubles + pwpos[e]] = (lv - 1.0) * ow;
+  }
 }
 
 // ll = sum(cs): Python's built-in sum, a left fold over the effects, by one
@@ -294,17 +321,29 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // c * ex and + 1.0 rounded separately, SVML log, and numpy's pairwise sum
 // over the wave as laid out by host::build_pairwise_plan.
 // ---------------------------------------------------------------------------
-// c is read from memory at every evaluation (an L2 / MALL-resident copy), so
-// no register holds it while the optimiser runs: kPlan, the plan-ordered copy
-// the fused kernel writes ([NS][17][64]: chain element m of slot u at row u *
-// 17 + m, the remainder at row 16, one coalesced row per element); else the
-// caller's [E] vector at the plan's indices.  The plan itself (per lane:
-// chain starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat, bool kPair = false>
+// c is read from memory at every evaluation, so no register holds it while
+// the optimiser runs: kPlan, the plan-ordered copy the fused kernel writes
+// ([NS][17][64]: chain element m of slot u at row u * 17 + m, the remainder
+// at row 16, one coalesced row per element); else the caller's [E] vector at
+// the plan's indices.  kRc (with kPlan): c recomputed at every evaluation from
+// the parent's plan-ordered a = (lv - 1) ow (the order weights' launch writes
+// them, one row set per (chain, parent k), shared by the S - 1 children of k)
+// and lv's bit -- c = a / ((1 - s a) + s (lv - 1)), nem_order_mcmc.py:161-164,
+// the same rounded operations -- so the objective reads 1.1 MB per chain
+// instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
+// starts, counts, remainders, tree partners) is the block's LDS copy.
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
   const double* cp;
+  // kRc: this lane's lv bits per slot (bit m: chain element m, bit 16: the
+  // remainder), s and s (lv - 1) of both values; pad_guard: a padding
+  // element's 1 + s (lo - 1) is 0 (s = 1, exp(lo) = 0), so its 0 / 0 is
+  // replaced by the 0 a stored row holds there
+  uint32_t rbits[kRc ? NS : 1];
+  double rs = 0.0, rslo = 0.0, rshi = 0.0;
+  bool pad_guard = false;
   const int32_t* pl;   // host::PairwisePlan rows in LDS: start, cnt, rem, nrem [NS][64], partner [8][64]
   int nh, maxrem, lane;
   double anc;
@@ -339,11 +378,21 @@ struct ExactObjective {
     return kRegs ? r_partner[kRegs ? h : 0] : pl[(4 * NS + h) * kWave + lane];
   }
 
+  __device__ __forceinline__ double rc_c(int u, int m, bool real) const {
+#pragma clang fp contract(off)
+    const double a = cp[(u * kRows + m) * kWave + lane];
+    const double sl = ((rbits[kRc ? u : 0] >> m) & 1u) ? rshi : rslo;
+    const double bd = (1.0 - rs * a) + sl;
+    const double c = a / bd;
+    return lb::uni(pad_guard) ? (real ? c : 0.0) : c;
+  }
   __device__ __forceinline__ double cval(int u, int m, int cu) const {
+    if (kRc) return rc_c(u, m, m < cu);
     if (kPlan) return cp[(u * kRows + m) * kWave + lane];
     return m < cu ? cp[start(u) + 8 * m] : 0.0;
   }
   __device__ __forceinline__ double crem(int u, int ru) const {
+    if (kRc) return rc_c(u, kChain, ru >= 0);
     if (kPlan) return cp[(u * kRows + kChain) * kWave + lane];
     return ru >= 0 ? cp[ru] : 0.0;
   }
@@ -501,16 +550,65 @@ struct SeqSumArgs {
 constexpr int kExactWaves = 4;
 constexpr int kStateDoubles = (int)((sizeof(LbxState) + 7) / 8);
 
+// The local optima's c rows (both forms): the stored form writes c = a / b,
+// nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k])), once, into this
+// optimum's plan-ordered rows `rows` (`slots`: the slots this wave writes,
+// bit u); the recompute form instead points the objective at the parent's a
+// rows (xa, written by eval #1's order-weight launch) with s, s (lv - 1) and
+// the lane's lv bits
+struct CArgs {
+  const double* xa = nullptr;        // kRc: [chains][S][plan doubles]
+  const uint32_t* xbits = nullptr;   // kRc: [S][NS][64]
+  double* cbuf = nullptr;            // stored: [optima][plan doubles]
+  int xcd = 0;                       // XCD-contiguous optimum ranges (option exact_xcd)
+};
+template <class Obj, int NS, bool kRc>
+__device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E, int b, int k, size_t gw, double s,
+                                        double lvlo, double lvhi, const double* __restrict__ owk,
+                                        const uint64_t* __restrict__ d1w, int nwords, int lane, unsigned slots) {
+#pragma clang fp contract(off)
+  constexpr size_t kPlanD = (size_t)NS * Obj::kRows * kWave;
+  if (kRc) {
+    obj.cp = ca.xa + ((size_t)b * S + k) * kPlanD;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) obj.rbits[kRc ? u : 0] = ca.xbits[((size_t)k * NS + u) * kWave + lane];
+    obj.rs = s;
+    obj.rslo = s * (lvlo - 1.0);
+    obj.rshi = s * (lvhi - 1.0);
+    obj.pad_guard = 1.0 + obj.rslo == 0.0;
+    return;
+  }
+  auto cval = [&](int e) {
+#pragma clang fp contract(off)
+    const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
+    const double a = (lv - 1.0) * owk[e];
+    const double bd = (1.0 - s * a) + s * (lv - 1.0);
+    return a / bd;
+  };
+  double* rows = ca.cbuf + gw * kPlanD;
+  obj.cp = rows;
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    if (!((slots >> u) & 1u)) continue;
+    const int st = obj.start(u), ct = obj.cnt(u), re = obj.rem(u);
+    double* row = rows + u * Obj::kRows * kWave + lane;
+#pragma unroll 4
+    for (int m = 0; m < Obj::kChain; ++m) row[m * kWave] = m < ct ? cval(st + 8 * m) : 0.0;
+    row[Obj::kChain * kWave] = re >= 0 ? cval(re) : 0.0;
+  }
+  __threadfence_block();   // the rows are read back by the same lanes
+}
+
 // one wave per (chain, permissible pair), kExactWaves per block; then the
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
-template <int NS, bool kLat>
+template <int NS, bool kLat, bool kRc>
 __global__ __launch_bounds__(kExactWaves * kWave)
 __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_exact_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
     int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
-    int32_t* __restrict__ info, double* __restrict__ cbuf, int lo_blocks, SeqSumArgs fin) {
+    int32_t* __restrict__ info, CArgs ca, int lo_blocks, SeqSumArgs fin) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ double mem[kExactWaves][lbx::kMemDoubles];
@@ -530,7 +628,8 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   plan_to_lds<NS>(plan, nh, pl);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
-  const int gw = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
+  const int blk = xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks);
+  const int gw = __builtin_amdgcn_readfirstlane(blk * kExactWaves + wv);
   const int lane = threadIdx.x & (kWave - 1);
   if (gw >= nchains * npairs) return;  // uniform per wave
   const int b = gw / npairs;
@@ -540,9 +639,8 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   const int k = pk & 0xffff;
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
-  const double lvlo = xlo[k], lvhi = xhi[k];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
-  using Obj = ExactObjective<NS, true, kLat>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -551,26 +649,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   obj.maxrem = maxrem;
   obj.anc = anc[idx];
   obj.load_plan();
-  // c = a / b, nem_order_mcmc.py:161-164 (local_vec = np.exp(T[i][k])), once,
-  // into this wave's plan-ordered rows
-  auto cval = [&](int e) {
-#pragma clang fp contract(off)
-    const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
-    const double a = (lv - 1.0) * owk[e];
-    const double bd = (1.0 - s * a) + s * (lv - 1.0);
-    return a / bd;
-  };
-  double* rows = cbuf + (size_t)gw * NS * Obj::kRows * kWave;
-  obj.cp = rows;
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {
-    const int st = obj.start(u), ct = obj.cnt(u), re = obj.rem(u);
-    double* row = rows + u * Obj::kRows * kWave + lane;
-#pragma unroll 4
-    for (int m = 0; m < Obj::kChain; ++m) row[m * kWave] = m < ct ? cval(st + 8 * m) : 0.0;
-    row[Obj::kChain * kWave] = re >= 0 ? cval(re) : 0.0;
-  }
-  __threadfence_block();   // the rows are read back by the same lanes
+  setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
   while (lbx_run(st, lbx::Mem{mem[wv]})) {
@@ -597,13 +676,13 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
 // same optimiser on their own copy of its state, so they take the same path
 // and the same number of barriers.  Appended blocks as above (two chains per
 // block).
-template <int NS>
+template <int NS, bool kRc>
 __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4))) void local_opt_exact_pair_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
     int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew, double* __restrict__ wdag,
-    int32_t* __restrict__ info, double* __restrict__ cbuf, int lo_blocks, SeqSumArgs fin) {
+    int32_t* __restrict__ info, CArgs ca, int lo_blocks, SeqSumArgs fin) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ double mem[2][lbx::kMemDoubles];
@@ -621,7 +700,7 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
   }
   tabs.fill(threadIdx.x, blockDim.x);
   __syncthreads();
-  const int gw = blockIdx.x;   // the optimum: uniform over the block
+  const int gw = xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks);   // the optimum: uniform over the block
   if (gw >= nchains * npairs) return;
   const int b = gw / npairs;
   const int n = gw - b * npairs;
@@ -630,12 +709,11 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
   const int k = pk & 0xffff;
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
-  const double lvlo = xlo[k], lvhi = xhi[k];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   // the throughput form's objective (few registers: four waves per SIMD
   // hold the 2 x 2016 waves of one chain's step), its plan in registers
   // (read once from global memory: no LDS copy, so eight blocks fit a CU)
-  using Obj = ExactObjective<NS, true, false, true>;
+  using Obj = ExactObjective<NS, true, false, true, kRc>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = plan;
@@ -646,25 +724,9 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
   obj.xres = xres;
   obj.half = wv;
   obj.load_plan();
-  auto cval = [&](int e) {
-#pragma clang fp contract(off)
-    const double lv = d1bit(d1w, nwords, k, e) ? lvhi : lvlo;
-    const double a = (lv - 1.0) * owk[e];
-    const double bd = (1.0 - s * a) + s * (lv - 1.0);
-    return a / bd;
-  };
-  double* rows = cbuf + (size_t)gw * NS * Obj::kRows * kWave;
-  obj.cp = rows;
-#pragma unroll
-  for (int u = 0; u < NS; ++u) {   // this wave's slots' rows (it alone reads them)
-    if ((u & 1) != wv) continue;
-    const int st = obj.start(u), ct = obj.cnt(u), re = obj.rem(u);
-    double* row = rows + u * Obj::kRows * kWave + lane;
-#pragma unroll 4
-    for (int m = 0; m < Obj::kChain; ++m) row[m * kWave] = m < ct ? cval(st + 8 * m) : 0.0;
-    row[Obj::kChain * kWave] = re >= 0 ? cval(re) : 0.0;
-  }
-  __threadfence_block();
+  // this wave's slots' rows (it alone reads them)
+  setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane,
+                        wv ? 0xaaaaaaaau : 0x55555555u);
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
   while (lbx_run(st, lbx::Mem{mem[wv]})) {
@@ -773,6 +835,10 @@ hipError_t launch_local_opt_exact_generic(Ctx& c, int n, const double* d_c, cons
     NEMO_EXACT_NS(2)
     NEMO_EXACT_NS(3)
     NEMO_EXACT_NS(4)
+    NEMO_EXACT_NS(5)
+    NEMO_EXACT_NS(6)
+    NEMO_EXACT_NS(7)
+    NEMO_EXACT_NS(8)
 #undef NEMO_EXACT_NS
     default:
       return hipErrorInvalidValue;
@@ -787,17 +853,18 @@ hipError_t launch_refmath_probe(int fn, int n, const double* d_x, const double* 
 
 bool exact_supported(const Ctx& c) { return c.factored && c.exact_ok && c.d_xlo && c.d_pwplan; }
 
-size_t exact_cbuf_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true, true>::kRows * kWave); }
+size_t exact_plan_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true, true>::kRows * kWave); }
 
-hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
-                             double* d_cs, double* d_ll, bool want_ow, hipStream_t st) {
+hipError_t launch_exact_eval(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, double* d_cells,
+                             double* d_cs, double* d_ll, bool want_ow, hipStream_t st, double* d_xa) {
   const int S = c.S, E = c.E;
   // one wave per group of 4 D1 words, at most kCellsThreads / 64 waves; 8
   // children per block once the batch alone fills the chip
   const int cw = std::min(kCellsThreads / kWave, std::max(1, (c.nwords + 3) / 4));
   const int rows = batch >= 512 ? std::min(kCellsRows, kCellsSlots / S) : 1;
   const int nchunk = (S + rows) / rows;
-  exact_cells_kernel<<<dim3(batch * nchunk), cw * kWave, 0, st>>>(S, E, rows, d_pos, d_w01, c.d_xlo, c.d_xhi,
+  exact_cells_kernel<<<dim3(batch * nchunk), cw * kWave, 0, st>>>(S, E, rows, cap >= S - 1 ? 0 : cap, d_pos, d_w01,
+                                                                  c.d_xlo, c.d_xhi,
                                                                   c.d_D1w, c.nwords, c.d_U64, d_cells);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
@@ -807,7 +874,9 @@ hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const doub
   err = hipGetLastError();
   if (err == hipSuccess && want_ow) {
     const size_t ncell = (size_t)batch * (S + 1) * E;
-    exact_ow_kernel<<<(unsigned)((ncell + 255) / 256), 256, 0, st>>>(S, E, batch, d_cells, d_cs);
+    exact_ow_kernel<<<(unsigned)((ncell + 255) / 256), 256, 0, st>>>(
+        S, E, batch, d_cells, d_cs, d_xa, c.d_pwpos, (int)exact_plan_doubles(c), c.d_xlo, c.d_xhi, c.d_D1w,
+        c.nwords);
     err = hipGetLastError();
   }
   if (err != hipSuccess || !d_ll) return err;
@@ -815,59 +884,82 @@ hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const doub
   return hipGetLastError();
 }
 
+namespace {
+
+struct LoArgs {
+  int S, E, npairs, nchains;
+  const int32_t* pairs;
+  const double *w01, *anc, *ow, *xlo, *xhi;
+  const uint64_t* d1w;
+  int nwords;
+  const int32_t* plan;
+  int nh, maxrem;
+  double sig0, sig1;
+  double *wnew, *wdag;
+  int32_t* info;
+  CArgs ca;
+  int lo_blocks;
+  SeqSumArgs fin;
+};
+
+template <int NS, bool kRc>
+void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
+  if (form == 3)
+    local_opt_exact_pair_kernel<NS, kRc><<<grid, 2 * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+  else if (form == 1)
+    local_opt_exact_kernel<NS, true, kRc><<<grid, kExactWaves * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+  else
+    local_opt_exact_kernel<NS, false, kRc><<<grid, kExactWaves * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+}
+
+template <int NS>
+void launch_lo_ns(const LoArgs& a, int form, bool rc, dim3 grid, hipStream_t st) {
+  if (rc) launch_lo<NS, true>(a, form, grid, st);
+  else launch_lo<NS, false>(a, form, grid, st);
+}
+
+}  // namespace
+
 hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t* d_pairs, const double* d_w01,
                                   const double* d_anc, const double* d_ow, double sig0, double sig1, double* d_wnew,
                                   double* d_wdag, int32_t* d_info, const double* d_cs1, double* d_ll1,
                                   hipStream_t st) {
   const int nw = nchains * npairs;
-  if ((size_t)nw * exact_cbuf_doubles(c) > c.cap_xcbuf) return hipErrorInvalidValue;
-  const int lo_blocks = (nw + kExactWaves - 1) / kExactWaves;
-  SeqSumArgs fin{d_cs1, c.E, nchains, d_ll1};
-  const int fin_blocks = d_ll1 ? (nchains + kExactWaves - 1) / kExactWaves : 0;
-  const dim3 grid(lo_blocks + fin_blocks);
+  const bool rc = c.exact_cform == 1;
+  if (rc ? (size_t)nchains * c.S * exact_plan_doubles(c) > c.cap_xa
+         : (size_t)nw * exact_plan_doubles(c) > c.cap_xcbuf)
+    return hipErrorInvalidValue;
   // the latency form while the optima fit in two waves per SIMD (the GPU's
   // 256 CUs x 4 SIMDs); the throughput form (four per SIMD) beyond; the pair
-  // form (option exact_form 3) for few optima with two slots or more
-  const bool lat = c.exact_form == 1 || (c.exact_form == 0 && nw <= c.exact_lat_waves);
-  const bool pair = c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves));
-  if (pair) {
-    const int pfin = d_ll1 ? (nchains + 1) / 2 : 0;
-    const dim3 pgrid(nw + pfin);
-    switch (c.pw_ns) {
-#define NEMO_EXACT_PAIR(NSV)                                                                                     \
-  case NSV:                                                                                                      \
-    local_opt_exact_pair_kernel<NSV><<<pgrid, 2 * kWave, 0, st>>>(                                             \
-        c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
-        c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, nw, fin);                           \
-    break;
-      NEMO_EXACT_PAIR(2)
-      NEMO_EXACT_PAIR(3)
-      NEMO_EXACT_PAIR(4)
-#undef NEMO_EXACT_PAIR
-      default:
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
+  // form for few optima with two slots or more
+  int form = c.exact_form;
+  if (form == 0) form = nw <= c.exact_lat_waves ? 1 : 2;
+  if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves))) form = 3;
+  if (c.pw_ns < 2 && form == 3) form = 2;
+  const int lo_blocks = form == 3 ? nw : (nw + kExactWaves - 1) / kExactWaves;
+  const int per_fin = form == 3 ? 2 : kExactWaves;   // waves per appended block
+  const int fin_blocks = d_ll1 ? (nchains + per_fin - 1) / per_fin : 0;
+  LoArgs a{c.S,     c.E,      npairs,  nchains,  d_pairs,  d_w01,    d_anc,    d_ow,     c.d_xlo,
+           c.d_xhi, c.d_D1w,  c.nwords, c.d_pwplan, c.pw_nh, c.pw_maxrem, sig0,  sig1,     d_wnew,
+           d_wdag,  d_info,   CArgs{c.d_xa, c.d_xbits, c.d_xcbuf, c.exact_xcd}, lo_blocks,
+           SeqSumArgs{d_cs1, c.E, nchains, d_ll1}};
+  const dim3 grid(lo_blocks + fin_blocks);
   switch (c.pw_ns) {
-#define NEMO_EXACT_NS(NSV)                                                                                         \
-  case NSV:                                                                                                        \
-    if (lat)                                                                                                       \
-      local_opt_exact_kernel<NSV, true><<<grid, kExactWaves * kWave, 0, st>>>(                                    \
-          c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
-          c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                    \
-    else                                                                                                           \
-      local_opt_exact_kernel<NSV, false><<<grid, kExactWaves * kWave, 0, st>>>(                                   \
-          c.S, c.E, npairs, nchains, d_pairs, d_w01, d_anc, d_ow, c.d_xlo, c.d_xhi, c.d_D1w, c.nwords, c.d_pwplan, \
-          c.pw_nh, c.pw_maxrem, sig0, sig1, d_wnew, d_wdag, d_info, c.d_xcbuf, lo_blocks, fin);                    \
-    break;
-    NEMO_EXACT_NS(1)
-    NEMO_EXACT_NS(2)
-    NEMO_EXACT_NS(3)
-    NEMO_EXACT_NS(4)
-#undef NEMO_EXACT_NS
-    default:
-      return hipErrorInvalidValue;
+    case 1: launch_lo_ns<1>(a, form, rc, grid, st); break;
+    case 2: launch_lo_ns<2>(a, form, rc, grid, st); break;
+    case 3: launch_lo_ns<3>(a, form, rc, grid, st); break;
+    case 4: launch_lo_ns<4>(a, form, rc, grid, st); break;
+    case 5: launch_lo_ns<5>(a, form, rc, grid, st); break;
+    case 6: launch_lo_ns<6>(a, form, rc, grid, st); break;
+    case 7: launch_lo_ns<7>(a, form, rc, grid, st); break;
+    case 8: launch_lo_ns<8>(a, form, rc, grid, st); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

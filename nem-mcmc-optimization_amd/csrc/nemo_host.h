@@ -184,6 +184,36 @@ inline bool build_pairwise_plan(int E, PairwisePlan& pl) {
   return true;
 }
 
+// Where each element e sits in a plan-ordered row set ([ns][17][64] doubles:
+// chain element m of slot u on lane l at (u * 17 + m) * 64 + l, the lane's
+// trailing element at row 16): pos[e], every e < E exactly once.
+inline void plan_positions(const PairwisePlan& pl, std::vector<int32_t>& pos) {
+  pos.assign((size_t)pl.E, -1);
+  for (int u = 0; u < pl.ns; ++u)
+    for (int l = 0; l < 64; ++l) {
+      const size_t q = (size_t)u * 64 + l;
+      for (int m = 0; m < pl.cnt[q]; ++m) pos[(size_t)pl.start[q] + 8 * m] = (u * 17 + m) * 64 + l;
+      if (pl.rem[q] >= 0) pos[(size_t)pl.rem[q]] = (u * 17 + 16) * 64 + l;
+    }
+}
+
+// The D1 bit of parent row k at each lane's plan elements: bits[(k * ns + u)
+// * 64 + l], bit m = element m of the lane's chain in slot u, bit 16 = its
+// trailing element (0 where there is none)
+inline void plan_lv_bits(const PairwisePlan& pl, int S, const uint64_t* d1, int nwords, std::vector<uint32_t>& bits) {
+  bits.assign((size_t)S * pl.ns * 64, 0u);
+  auto bit = [&](int k, long e) { return (uint32_t)((d1[(size_t)k * nwords + e / 64] >> (e % 64)) & 1ull); };
+  for (int k = 0; k < S; ++k)
+    for (int u = 0; u < pl.ns; ++u)
+      for (int l = 0; l < 64; ++l) {
+        const size_t q = (size_t)u * 64 + l;
+        uint32_t w = 0;
+        for (int m = 0; m < pl.cnt[q]; ++m) w |= bit(k, (long)pl.start[q] + 8 * m) << m;
+        if (pl.rem[q] >= 0) w |= bit(k, pl.rem[q]) << 16;
+        bits[((size_t)k * pl.ns + u) * 64 + l] = w;
+      }
+}
+
 // the two addition chains of compute_scores (nem.py:25-34), in its order:
 // chains[k] = 0 + A + ... (k times), chains[S + 1 + k] = B + A + ... (k times)
 inline std::vector<double> knockdown_chains(int S, double A, double B) {

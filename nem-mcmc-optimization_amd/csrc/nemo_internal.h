@@ -21,6 +21,7 @@ constexpr int kFactWaves = 8;      // waves per factored-score block (16 effects
 constexpr int kI8MaxPairs = 5;     // digit-slice pairs of the int8 factored kernel
 constexpr int kWinMaxCap = 6;      // capped lookup-table kernel: parents per child
 constexpr int kWinMaxS = kMaxS;    // ... and S (LDS: ~356 S bytes per block)
+constexpr int kExactMaxSlots = 8;  // exact local optima: numpy's pairwise sum of E in <= 64 leaf blocks (E <= 8192)
 
 // Device state of one staged model on one GPU.
 struct Ctx {
@@ -127,9 +128,20 @@ struct Ctx {
   int32_t* d_pwplan = nullptr;     // host::PairwisePlan of E, device layout
   int pw_ns = 0, pw_nh = 0, pw_maxrem = 0;
   double* d_xcs = nullptr;         // [2][chains][E] cs of the step's two evaluations
-  double* d_xcells2 = nullptr;     // [chains][S+1][E] eval #2's cells
-  double* d_xcbuf = nullptr;       // [chains * pairs][exact_cbuf_doubles] the local optima's c, plan order
-  size_t cap_xcbuf = 0;            // its size in doubles
+  double* d_xcells2 = nullptr;     // [chains][S+1][E] eval #2's cells (allocated on first use)
+  size_t cap_xcells2 = 0;          // its chains
+  double* d_xcbuf = nullptr;       // [chains * pairs][exact_plan_doubles] the local optima's c, plan order
+  size_t cap_xcbuf = 0;            // its size in doubles (allocated on first use of the stored form)
+  // the local optima's c: option "exact_cform" 0 = stored (c = a / b written
+  // once per optimum into d_xcbuf, read at every evaluation), 1 = recomputed at
+  // every evaluation from the parent's plan-ordered a = (lv - 1) ow (d_xa,
+  // written by eval #1's order-weight launch) and lv's bit (d_xbits)
+  int exact_cform = 1;
+  int exact_xcd = 1;               // option "exact_xcd": XCD-contiguous optimum ranges
+  double* d_xa = nullptr;          // [chains][S][exact_plan_doubles]
+  size_t cap_xa = 0;               // its size in doubles
+  uint32_t* d_xbits = nullptr;     // [S][pw_ns][64] lv bit of parent row k per (slot, lane): bit m, 16 = remainder
+  int32_t* d_pwpos = nullptr;      // [E] plan position (u * 17 + m) * 64 + lane of element e
 
   // worst-case |ll error| of the fixed-point kernels (nemo_host.h):
   // fx_colsum[k] = sum_e min(colbits_e, k) over the staged D1 bits; auto takes
@@ -238,12 +250,14 @@ hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const doub
 
 // the reference's arithmetic (nemo_exact.hip): supported for this staging?
 bool exact_supported(const Ctx& c);
-size_t exact_cbuf_doubles(const Ctx& c);   // per local optimum
+size_t exact_plan_doubles(const Ctx& c);   // one plan-ordered row set (per optimum / per parent row)
 // eval in the reference's order: cells into d_cells [batch][S+1][E] (with
 // want_ow: replaced by the order weights), cs into d_cs [batch][E], ll into
 // d_ll (nullable: left to the caller)
-hipError_t launch_exact_eval(Ctx& c, int batch, const int32_t* d_pos, const double* d_w01, double* d_cells,
-                             double* d_cs, double* d_ll, bool want_ow, hipStream_t st);
+// d_xa (with want_ow): also a = (lv - 1) ow of rows 0..S-1 in plan order
+// (cap: the parent-set cap, 0 none, as the score kernels)
+hipError_t launch_exact_eval(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, double* d_cells,
+                             double* d_cs, double* d_ll, bool want_ow, hipStream_t st, double* d_xa = nullptr);
 // every permissible pair's exact local optimum; the appended blocks sum d_cs1
 // into d_ll1 (eval #1's ll) when d_ll1 is set
 hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t* d_pairs, const double* d_w01,

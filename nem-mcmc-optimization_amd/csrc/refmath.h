@@ -21,6 +21,14 @@
 //
 // Header-only, host and device (hipcc) or host only (g++ with
 // -ffp-contract=off: every fused operation below is an explicit fma()).
+//
+// Attribution: the algorithms restated here are glibc 2.35's exp (Szabolcs
+// Nagy, Arm; LGPL-2.1-or-later) and log1p (fdlibm, Sun Microsystems: "Developed
+// at SunPro, a Sun Microsystems, Inc. business. Permission to use, copy,
+// modify, and distribute this software is freely granted, provided that this
+// notice is preserved."), and Intel SVML's log / exp kernels as bundled in
+// numpy (BSD-3-Clause, Intel Corporation).  No library source is copied; see
+// THIRD_PARTY_NOTICES.md.
 #pragma once
 
 #include <stdint.h>

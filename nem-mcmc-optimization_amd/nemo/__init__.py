@@ -9,7 +9,7 @@ of ``include/nemo.h`` (``libnemo.so``, loaded with ctypes).
 from . import generator, utils
 from .nem import NEM
 
-__all__ = ["NEM", "generator", "utils", "Engine", "NEMOrderMCMC"]
+__all__ = ["NEM", "generator", "utils", "Engine", "NEMOrderMCMC", "ExactArithmeticWarning"]
 
 
 def __getattr__(name):
@@ -17,6 +17,9 @@ def __getattr__(name):
     if name == "Engine":
         from .engine import Engine
         return Engine
+    if name == "ExactArithmeticWarning":
+        from .engine import ExactArithmeticWarning
+        return ExactArithmeticWarning
     if name == "NEMOrderMCMC":
         from .nem_order_mcmc import NEMOrderMCMC
         return NEMOrderMCMC

@@ -18,6 +18,12 @@ from ._lib import check, f64, i32, ptr
 _DTYPES = {"f64": _lib.NEMO_F64, "f32": _lib.NEMO_F32}
 
 
+class ExactArithmeticWarning(UserWarning):
+    """The staged model is outside what the reference-arithmetic kernels
+    cover, so the sampler's step runs the fast kernels: log-scores within
+    1e-6 of the reference's, not its bits."""
+
+
 class Engine:
     """Staged model on one GPU.
 
@@ -233,6 +239,20 @@ class Engine:
         check(_lib.load().nemo_score_kernel(self._ctx, int(cap), 1 if ll_only else 0, C.byref(fk),
                                             C.byref(b)))
         return fk.value, b.value
+
+    def exact_status(self):
+        """(True, "") when the fused step and the sampler's score calls run in
+        the reference's own arithmetic (option ``exact``, the default, on a
+        model the exact kernels cover); else (False, the reason)."""
+        if not self.get_option("exact"):
+            return False, "option exact is 0"
+        if not self.factored:
+            return False, ("the staged tables are not the factored form nem.py builds (every off-diagonal "
+                           "row shared by all children, two-valued)")
+        if not self.get_option("exact_ok"):
+            return False, (f"numpy's pairwise sum of E={self.E} effects needs more than 64 leaf blocks "
+                           "(the exact kernels' wave plan covers E <= 8192)")
+        return True, ""
 
     @property
     def factored(self) -> bool:

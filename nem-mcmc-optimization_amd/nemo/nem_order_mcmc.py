@@ -22,6 +22,7 @@ weights, which equals the score ``get_optimal_weights`` just produced.
 from __future__ import annotations
 
 import random
+import warnings
 from itertools import cycle
 
 import numpy as np
@@ -29,7 +30,7 @@ from scipy.linalg import inv
 from scipy.special import expit
 
 from . import utils
-from .engine import Engine, lse_full
+from .engine import Engine, ExactArithmeticWarning, lse_full
 from ._lib import LBFGSB_ABNORMAL
 
 SIG0 = float(expit(0.0))   # expit of a binarised "no edge" weight
@@ -85,13 +86,15 @@ class NEMOrderMCMC:
     rng = random
 
     def __init__(self, nem, perm_order, device: int = 0, dtype: str = "f64", cap: int = 0,
-                 engine: Engine | None = None):
+                 engine: Engine | None = None, strict: bool = False):
         """Reference: nem_order_mcmc.py:29-48.
 
         Extra keyword arguments (build-defined): ``device`` (GPU index),
         ``dtype`` ('f64' or the fp32 'f32' table path), ``cap`` (parent-set cap,
         0 = every predecessor, as in the reference), ``engine`` (share a staged
-        model between samplers)."""
+        model between samplers), ``strict`` (raise instead of warning when the
+        staged model is outside the reference-arithmetic kernels; an engine
+        whose option ``exact`` was set to 0 on purpose is not checked)."""
         self.nem = nem
         self.num_s = nem.num_s
         self.num_e = nem.num_e
@@ -101,6 +104,14 @@ class NEMOrderMCMC:
         self.score_tables = nem.get_score_tables(nem.observed_knockdown_mat)
         self.cap = int(cap)
         self.engine = engine if engine is not None else Engine.for_nem(nem, device=device, dtype=dtype)
+        if self.engine.get_option("exact"):
+            ok, why = self.engine.exact_status()
+            if not ok:
+                msg = (f"NEMOrderMCMC: {why}; the step runs the fast kernels (log-scores within 1e-6 of "
+                       "the reference's, not its bits)")
+                if strict:
+                    raise RuntimeError(msg)
+                warnings.warn(msg, ExactArithmeticWarning, stacklevel=2)
         self.get_permissible_parents(perm_order, init=True, init_value=1.0)
         self.cell_ratios = self.compute_cell_ratios(self.parent_weights, self.score_tables)
         self.perm_order = perm_order

@@ -222,10 +222,13 @@ class OracleSampler:
     """Restatement of ``NEMOrderMCMC`` with the documented ``opt_weights``
     pass-through.  Uses the global ``random`` stream, like the reference."""
 
-    def __init__(self, u, t, perm_order, record_local=False):
+    def __init__(self, u, t, perm_order, record_local=False, cap=0):
+        """``cap``: parent-set cap (the build-defined C5 extension: every
+        parent list is the last <= cap predecessors, as ``parents_of``)."""
         self.u = np.array(u, dtype=np.float64)
         self.t = t
         self.s = t.shape[0]
+        self.cap = int(cap)
         self.w = np.zeros((self.s, self.s))
         self.record_local = record_local
         self.local_log = []
@@ -242,7 +245,7 @@ class OracleSampler:
         parents = []
         for i in range(self.s):
             p = int(np.where(perm == i)[0][0])
-            pa = perm[:p]
+            pa = perm[max(0, p - self.cap) if self.cap else 0:p]
             parents.append(pa)
             if init:
                 for j in pa:

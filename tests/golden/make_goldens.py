@@ -7,7 +7,8 @@ documented ``opt_weights`` pass-through, and writes small
 ``.npz`` fixtures next to this script.  The fixtures are data (inputs and the
 reference's outputs); no reference source is stored.
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N | --only-traj-nem]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N | --only-traj-nem
+                                                          | --only-c3-extra]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -229,14 +230,19 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
         print(f"localopt_{name}: {len(local)} records")
 
 
-def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=4, seed=2024):
-    """replica_exchange_method (nem_order_mcmc.py:344-363) on net2: 10 replicas,
-    gamma_r = (1 + 0.2 r) S / E, `n_exchange` rounds of `n_iter` steps.  Each
-    round's replica_exchange_step result is recorded through a wrapper of the
-    module-level function (the reference itself runs unchanged)."""
-    adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
-    m = quiet(ref_nem.NEM, adj, end, err, s, e)
-    order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=4, seed=2024, model=None,
+                             name="net2"):
+    """replica_exchange_method (nem_order_mcmc.py:344-363) on net2 (or on the
+    given (model, order)): 10 replicas, gamma_r = (1 + 0.2 r) S / E,
+    `n_exchange` rounds of `n_iter` steps.  Each round's replica_exchange_step
+    result is recorded through a wrapper of the module-level function (the
+    reference itself runs unchanged)."""
+    if model is None:
+        adj, end, err, s, e = ref_utils.read_csv_to_adj(os.path.join(REF, "DAGs/networks/network2/network2.csv"))
+        m = quiet(ref_nem.NEM, adj, end, err, s, e)
+        order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
+    else:
+        m, order = model
     rounds = []
     orig = ref_mcmc.replica_exchange_step
 
@@ -255,7 +261,7 @@ def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=
     finally:
         ref_mcmc.replica_exchange_step = orig
     np.savez_compressed(
-        os.path.join(HERE, "replica_net2.npz"), seed=seed, n_exchange=n_exchange, n_iter=n_iter,
+        os.path.join(HERE, f"replica_{name}.npz"), seed=seed, n_exchange=n_exchange, n_iter=n_iter,
         order0=order, best_score=best_score, best_dag=np.asarray(best_nem.best_dag),
         best_order=np.asarray(best_nem.best_order),
         round_scores=np.array([r["scores"] for r in rounds]), round_nex=np.array([r["n_ex"] for r in rounds]),
@@ -390,6 +396,18 @@ def main():
         m = quiet(ref_nem.NEM, adj, end, err, s, e)
         order = ref_utils.initial_order_guess(m.observed_knockdown_mat)
         capture_traj(ref_mcmc, m, order, 2.0 * s / e, 0.90, 50, "net2_nem_50", use_nem=True)
+        return
+    if "--only-c3-extra" in sys.argv:
+        # the headline model (C3, 64 x 2000): replica_exchange_method with 10
+        # replicas, 2 exchange rounds of 3 steps, and a 20-step
+        # method(use_nem=True) trajectory (default swap_prob 0.95, gamma 2S/E)
+        net = gen.synthetic_network(64, 2000, 0)
+        mc3 = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, 64, 2000)
+        order3 = ref_utils.initial_order_guess(mc3.observed_knockdown_mat)
+        capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=2, n_iter=3, seed=2025,
+                                 model=(mc3, order3), name="C3")
+        random.seed(77)
+        capture_traj(ref_mcmc, mc3, order3, 2.0 * 64 / 2000, 0.95, 20, "C3_nem_20", use_nem=True)
         return
     if "--only-evals" in sys.argv:
         capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)

@@ -189,10 +189,12 @@ def test_exact_fused_step_equals_oracle_c3():
     eng.close()
 
 
-@pytest.mark.parametrize("e", [2600, 4096])
+@pytest.mark.parametrize("e", [2600, 3900, 4096, 4097, 5000])
 def test_exact_fused_step_equals_oracle_more_slots(e):
-    """E past 2048 (32 leaves of 128: four slots of the wave plan): one fused step in
-    the throughput and the pair forms against the oracle, to the bit."""
+    """E past 2048 (more than 16 leaf blocks of numpy's pairwise sum: 3 to 8
+    slots of the wave plan; 3900 and 4097 split into 33 leaves, 5000 into 64):
+    one fused step in the throughput and the pair forms, with c stored and
+    recomputed, against the oracle, to the bit."""
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m = generator.synthetic_nem(12, e, 3)
     eng = Engine.for_nem(m)
@@ -204,21 +206,106 @@ def test_exact_fused_step_equals_oracle_more_slots(e):
     ora = no.OracleSampler(m.U, t, perm)
     ora.w = w_raw.copy()
     ref_dag = ora.optimal_weights()
-    for form in (2, 3):
-        eng.set_option("exact_form", form)
-        smp = NEMOrderMCMC(m, perm, engine=eng)
-        smp.parent_weights = w_raw.copy()
-        got_dag = smp.get_optimal_weights(init=True)
-        assert smp.ll == ora.ll1 and got_dag == ref_dag, form
-        assert _bits_equal(smp.parent_weights, ora.w), form
-    eng.set_option("exact_form", 0)
+    try:
+        for form in (2, 3):
+            for cform in (0, 1):
+                eng.set_option("exact_form", form)
+                eng.set_option("exact_cform", cform)
+                smp = NEMOrderMCMC(m, perm, engine=eng)
+                smp.parent_weights = w_raw.copy()
+                got_dag = smp.get_optimal_weights(init=True)
+                assert smp.ll == ora.ll1 and got_dag == ref_dag, (form, cform)
+                assert _bits_equal(smp.parent_weights, ora.w), (form, cform)
+    finally:
+        eng.set_option("exact_form", 0)
+        eng.set_option("exact_cform", 1)
+        eng.close()
+
+
+def test_exact_capped_fused_step_equals_oracle_c5():
+    """C5's shape, 128 x 5000 with parent cap 6 (the build-defined cap: every
+    parent list the last <= 6 predecessors): one fused step against the oracle
+    with the same capped lists -- eval #1's ll, every weight and dag_ll to the
+    bit -- in both c forms."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.config_nem("C5")
+    eng = Engine.for_nem(m)
+    assert eng.get_option("exact_ok") == 1
+    t = m.get_score_tensor()
+    rng = np.random.default_rng(55)
+    perm = rng.permutation(m.num_s)
+    w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
+    ora = no.OracleSampler(m.U, t, perm, cap=6)
+    ora.w = w_raw.copy()
+    ref_dag = ora.optimal_weights()
+    try:
+        for cform in (1, 0):
+            eng.set_option("exact_cform", cform)
+            smp = NEMOrderMCMC(m, perm, engine=eng, cap=6)
+            smp.parent_weights = w_raw.copy()
+            got_dag = smp.get_optimal_weights(init=True)
+            assert smp.ll == ora.ll1 and got_dag == ref_dag, cform
+            assert _bits_equal(smp.parent_weights, ora.w), cform
+    finally:
+        eng.set_option("exact_cform", 1)
+        eng.close()
+
+
+def test_exact_capped_scores_equal_golden_c5():
+    """The capped order scores of the C5 golden (the reference's own
+    calculate_ll with parents_list cut to the last 6 predecessors,
+    tests/golden/make_goldens.py): ll and cs to the bit, through the
+    sampler's host path and the batched device entry (option exact_dev)."""
+    import torch
+    z = golden("eval_C5cap.npz")
+    m = generator.synthetic_nem(int(z["S"]), int(z["E"]), int(z["seed"]))
+    cap = int(z["cap"])
+    eng = Engine.for_nem(m)
+    pos = np.array([np.argsort(p) for p in z["perm"]], dtype=np.int32)
+    w01 = expit(z["W"])
+    r = eng.score(pos, w01, cap=cap, want_cs=True)
+    assert _bits_equal(r["ll"], z["ll"]) and _bits_equal(r["cs"], z["cs"])
+    eng.set_option("exact_dev", 1)
+    try:
+        b = pos.shape[0]
+        eng.reserve(b)
+        dpos, dw = torch.from_numpy(pos).cuda(), torch.from_numpy(w01).cuda()
+        dll = torch.zeros(b, dtype=torch.float64, device="cuda")
+        eng.score_dev(b, dpos.data_ptr(), dw.data_ptr(), dll.data_ptr(), cap=cap,
+                      stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert _bits_equal(dll.cpu().numpy(), z["ll"])
+    finally:
+        eng.set_option("exact_dev", 0)
+        eng.close()
+
+
+def test_exact_score_cells_and_order_weights_together():
+    """nemo_score asked for the cells AND the order weights in the exact
+    arithmetic (both through one call): the cells of a cells-only call and
+    the order weights of an ow-only call, to the bit; with option exact_dev
+    set too (the host path never routes through the device entry's
+    one-buffer refusal)."""
+    m = generator.synthetic_nem(16, 500, 0)
+    eng = Engine.for_nem(m)
+    rng = np.random.default_rng(21)
+    pos = np.array([rng.permutation(16) for _ in range(3)], dtype=np.int32)
+    w01 = expit(rng.uniform(-4, 4, (3, 16, 16)))
+    cells = eng.score(pos, w01, want_cells=True)["cells"]
+    ow = eng.score(pos, w01, want_ow=True)["ow"]
+    for dev in (0, 1):
+        eng.set_option("exact_dev", dev)
+        r = eng.score(pos, w01, want_cells=True, want_ow=True)
+        assert _bits_equal(r["cells"], cells) and _bits_equal(r["ow"], ow), dev
+    eng.set_option("exact_dev", 0)
     eng.close()
 
 
 def test_exact_kernel_forms_give_the_same_bits():
     """The local-optimum kernel's latency, throughput and pair forms (option
-    exact_form 1 / 2 / 3): the same weights, dag weights and lls, to the bit,
-    for one chain and for three."""
+    exact_form 1 / 2 / 3), c stored or recomputed (exact_cform 0 / 1), in
+    launch order or XCD-contiguous order (exact_xcd): the same weights, dag
+    weights and lls, to the bit, for one chain and for three."""
     from nemo.nem_order_mcmc import SIG0, SIG1
     m = generator.synthetic_nem(64, 2000, 0)
     eng = Engine.for_nem(m)
@@ -228,15 +315,23 @@ def test_exact_kernel_forms_give_the_same_bits():
         w = rng.uniform(-3, 3, (n, 64, 64))
         anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
         outs = []
-        for form in (1, 2, 3):
-            eng.set_option("exact_form", form)
-            r = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
-            outs.append([np.array(x, copy=True) for x in r])
+        try:
+            for form in (1, 2, 3):
+                for cform in (0, 1):
+                    for xcd in (0, 1):
+                        eng.set_option("exact_form", form)
+                        eng.set_option("exact_cform", cform)
+                        eng.set_option("exact_xcd", xcd)
+                        r = eng.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
+                        outs.append([np.array(x, copy=True) for x in r])
+        finally:
+            eng.set_option("exact_form", 0)
+            eng.set_option("exact_cform", 1)
+            eng.set_option("exact_xcd", 1)
         for o in outs[1:]:
             assert len(o) == len(outs[0])
             for a, b in zip(outs[0], o):
                 assert _bits_equal(a, b)
-    eng.set_option("exact_form", 0)
     eng.close()
 
 
@@ -257,3 +352,38 @@ def test_exact_chain_batch_equals_single_chains():
         assert b1 == best[c]
         assert _bits_equal(smp.parent_weights, cb.chains[c].parent_weights)
     eng.close()
+
+
+def test_exact_fallback_is_loud():
+    """A model outside the exact kernels (E = 9000: numpy's pairwise sum in 128
+    leaf blocks; generic, non-factored tables) reports exact_ok 0, and the
+    sampler says so: a warning, or with strict=True an error.  A covered model
+    constructs silently."""
+    import warnings
+    from nemo.engine import ExactArithmeticWarning
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    m = generator.synthetic_nem(6, 9000, 1)
+    eng = Engine.for_nem(m)
+    assert eng.get_option("exact_ok") == 0 and eng.exact_status()[0] is False
+    perm = np.arange(6)
+    with pytest.warns(ExactArithmeticWarning, match="64 leaf blocks"):
+        NEMOrderMCMC(m, perm, engine=eng)
+    with pytest.raises(RuntimeError, match="fast kernels"):
+        NEMOrderMCMC(m, perm, engine=eng, strict=True)
+    eng.close()
+    m = generator.synthetic_nem(6, 300, 1)
+    rng = np.random.default_rng(2)
+    gen_eng = Engine(m.U, rng.normal(0, 1, (6, 6, 300)))   # not the factored form
+    assert gen_eng.get_option("exact_ok") == 0
+    with pytest.raises(RuntimeError, match="factored"):
+        NEMOrderMCMC(m, perm, engine=gen_eng, strict=True)
+    gen_eng.close()
+    ok_eng = Engine.for_nem(m)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        NEMOrderMCMC(m, perm, engine=ok_eng, strict=True)
+    ok_eng.set_option("exact", 0)          # chosen on purpose: not checked
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        NEMOrderMCMC(m, perm, engine=ok_eng, strict=True)
+    ok_eng.close()

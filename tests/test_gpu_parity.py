@@ -74,14 +74,23 @@ def test_score_synthetic_golden(name, s, e):
     assert np.array_equal(m.observed_knockdown_mat, _unpack_d(z))
     eng = Engine.for_nem(m)
     pos, w01 = _golden_batch(z)
-    out = eng.score(pos, w01, want_cs=True, want_ow=True)
-    assert np.max(np.abs(out["ll"] - z["ll"])) <= LL_TOL
-    # ll-only calls take the int8 offset kernel (U folded into the contraction)
-    assert eng.get_option("i8o") == 2
-    assert np.max(np.abs(eng.score(pos, w01) - z["ll"])) <= LL_TOL
-    assert np.max(np.abs(out["cs"] - z["cs"])) <= 1e-9
-    assert np.max(np.abs(out["ow"][0] - z["ow0"])) <= 1e-11
-    np.testing.assert_allclose(out["ow"].sum(axis=1), 1.0, atol=1e-12)
+    # the fast kernels (option exact 0; the default exact arithmetic gives the
+    # goldens' bits: test_gpu_exact.py)
+    eng.set_option("exact", 0)
+    try:
+        out = eng.score(pos, w01, want_cs=True, want_ow=True)
+        assert np.max(np.abs(out["ll"] - z["ll"])) <= LL_TOL
+        # ll-only calls take the int8 log2 offset kernel (U folded into the
+        # contraction): fact_kernel 10, within its own error bound
+        assert eng.get_option("i8o") == 2
+        fk, bound = eng.score_kernel(0, True)
+        assert fk == 10 and bound <= 1e-7
+        assert np.max(np.abs(eng.score(pos, w01) - z["ll"])) <= min(LL_TOL, bound)
+        assert np.max(np.abs(out["cs"] - z["cs"])) <= 1e-9
+        assert np.max(np.abs(out["ow"][0] - z["ow0"])) <= 1e-11
+        np.testing.assert_allclose(out["ow"].sum(axis=1), 1.0, atol=1e-12)
+    finally:
+        eng.set_option("exact", 1)
 
 
 def test_score_c5_cap6_f64_and_f32():
@@ -191,27 +200,30 @@ def test_fused_step_vs_oracle_c3(c3_model):
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m, eng = c3_model
     eng.set_option("exact", 0)
-    t = m.get_score_tensor()
-    rng = np.random.default_rng(12)
-    perm = rng.permutation(m.num_s)
-    smp = NEMOrderMCMC(m, perm, engine=eng)
-    w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
-    smp.parent_weights = w_raw.copy()
-    ora = _oracle_step_inputs(m.U, t, perm, w_raw)
-    ref_dag = ora.optimal_weights()
-    got_dag = smp.get_optimal_weights(init=True)
-    assert abs(smp.ll - ora.ll1) <= LL_TOL
-    mask = smp._mask
-    assert np.array_equal(smp.parent_weights[~mask], ora.w[~mask])
-    dw = np.abs(smp.parent_weights[mask] - ora.w[mask])
-    # 16 of the 2016 optima differ from scipy's by more than 1e-6 (max 8.5e-3,
-    # tools/parity_stats.py): the order weights differ from numpy's in the
-    # last bits and the forward-difference gradient (h = 1e-8) amplifies that
-    # into another line-search path; every binarised weight is the same
-    assert int((dw > 1e-6).sum()) <= 16 and dw.max() <= 1e-2
-    assert np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
-    assert abs(got_dag - ref_dag) <= LL_TOL
-    eng.set_option("exact", 1)
+    try:
+        t = m.get_score_tensor()
+        rng = np.random.default_rng(12)
+        perm = rng.permutation(m.num_s)
+        smp = NEMOrderMCMC(m, perm, engine=eng)
+        w_raw = rng.uniform(-3, 3, (m.num_s, m.num_s))
+        smp.parent_weights = w_raw.copy()
+        ora = _oracle_step_inputs(m.U, t, perm, w_raw)
+        ref_dag = ora.optimal_weights()
+        got_dag = smp.get_optimal_weights(init=True)
+        assert abs(smp.ll - ora.ll1) <= LL_TOL
+        mask = smp._mask
+        assert np.array_equal(smp.parent_weights[~mask], ora.w[~mask])
+        dw = np.abs(smp.parent_weights[mask] - ora.w[mask])
+        # 16 of the 2016 optima differ from scipy's by more than 1e-6 (max
+        # 8.5e-3, tools/parity_stats.py): the order weights differ from
+        # numpy's in the last bits and the forward-difference gradient (h =
+        # 1e-8) amplifies that into another line-search path; every binarised
+        # weight is the same
+        assert int((dw > 1e-6).sum()) <= 16 and dw.max() <= 1e-2
+        assert np.array_equal(smp.parent_weights[mask] > 0.5, ora.w[mask] > 0.5)
+        assert abs(got_dag - ref_dag) <= LL_TOL
+    finally:
+        eng.set_option("exact", 1)
 
 
 def _run_sampler(m, order, gamma, swap_prob, n, state):
@@ -559,6 +571,16 @@ def test_int8_kernel_bits_independent_of_split(c3_model):
     (and sums its partials in-kernel when one block owns it); ll bits must not
     depend on the batch size."""
     m, eng = c3_model
+    try:
+        _split_checks(m, eng)
+    finally:
+        # the module's engine back to its defaults, whatever failed
+        eng.set_option("fact_kernel", 0)
+        eng.set_option("score_path", 0)
+        eng.set_option("exact", 1)
+
+
+def _split_checks(m, eng):
     s = m.num_s
     rng = np.random.default_rng(21)
     b = 300
@@ -647,6 +669,61 @@ def test_replica_exchange_net2_golden(net2):
     assert abs(best2 - float(z["best_score"])) <= LL_TOL
     assert np.array_equal(nem2.best_order, z["best_order"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_replica_exchange_c3_golden():
+    """replica_exchange_method at the headline model (C3, 64 x 2000; make_goldens.py
+    --only-c3-extra): 10 replicas, 2 exchange rounds of 3 steps, global stream
+    seeded 2025.  The batched version and the sequential mirror reproduce the
+    reference's per-round scores and exchanges, the final best score, order and
+    DAG and the random state -- to the bit (option exact, the default)."""
+    from nemo import nem_order_mcmc as mc
+    from nemo.replicas import ReplicaExchange
+    z = golden("replica_C3.npz")
+    m = generator.synthetic_nem(64, 2000, 0)
+    order = utils.initial_order_guess(m.observed_knockdown_mat)
+    assert np.array_equal(order, z["order0"])
+    n_ex, n_it = int(z["n_exchange"]), int(z["n_iter"])
+    random.seed(int(z["seed"]))
+    rx = ReplicaExchange(m, order)
+    for k in range(n_ex):
+        best, best_obj, nx = rx.step(n_it, k % 2 == 0)
+        assert np.array_equal(rx.scores, z["round_scores"][k]), k
+        assert nx == int(z["round_nex"][k])
+        assert best == float(z["round_best"][k])
+        assert np.array_equal(np.array([np.asarray(rx.objs[r].best_order) for r in rx.obj_at_pos]),
+                              z["round_best_orders"][k])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    win = rx.objs[best_obj]
+    assert np.array_equal(win.best_order, z["best_order"]) and np.array_equal(win.best_dag, z["best_dag"])
+    random.seed(int(z["seed"]))
+    best2, nem2 = mc.replica_exchange_method(m, n_ex, n_it, order)
+    assert best2 == float(z["best_score"])
+    assert np.array_equal(nem2.best_order, z["best_order"]) and np.array_equal(nem2.best_dag, z["best_dag"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_trajectory_c3_use_nem_20():
+    """method(use_nem=True) at the headline model (C3; make_goldens.py
+    --only-c3-extra, global stream seeded 77): the transitive-closure DAG of
+    eval #2 and the accept step, 20 steps -- identical proposals and accepts,
+    every score, the best score, order and (closure) DAG, the final weights
+    and the random state, to the bit."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC
+    z = golden("traj_C3_nem_20.npz")
+    assert bool(z["use_nem"])
+    m = generator.synthetic_nem(64, 2000, 0)
+    random.seed(77)
+    smp = NEMOrderMCMC(m, z["order0"])
+    best, best_dag = smp.method(n_iterations=int(z["n_iter"]), gamma=float(z["gamma"]),
+                                swap_prob=float(z["swap_prob"]), verbose=False, use_nem=True)
+    assert np.array_equal(np.array(smp.accepted), z["acc"])
+    assert np.array_equal(np.array(smp.all_score_list), z["all_scores"])
+    assert best == float(z["best_score"])
+    assert np.array_equal(smp.best_order, z["best_order"])
+    assert np.array_equal(np.asarray(best_dag), z["best_dag"])
+    assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+    assert np.array_equal(smp.parent_weights, z["final_W"])
 
 
 def test_integration_stub_binds_the_library(net2):

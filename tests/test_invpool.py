@@ -72,3 +72,22 @@ def test_pool_prepare_bits_equal(pool):
     with pytest.raises(RuntimeError):
         pool.start(_mats(2, 16, 0))
         pool.finish_prepare()
+
+
+def test_default_workers_under_local_world_size(monkeypatch):
+    """default_workers: the cores this rank may use, shared by the node's
+    LOCAL_WORLD_SIZE ranks, one left for the rank itself, at least 1, capped
+    at 8 -- e.g. the 8-rank C4 run on a 256-core host gets 8 workers per rank
+    (64 helpers in all), on a 64-core host 7, on 16 cores 1."""
+    import os
+
+    from nemo import invpool
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    for cores, want in ((256, 8), (64, 7), (16, 1), (8, 1), (4, 1)):
+        monkeypatch.setattr(os, "sched_getaffinity", lambda pid, n=cores: set(range(n)))
+        assert invpool.default_workers() == want, cores
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(12)))
+    assert invpool.default_workers() == 8
+    assert invpool.default_workers(cap=4) == 4
+    assert invpool.default_workers(local_world=3) == 3

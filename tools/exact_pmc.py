@@ -16,7 +16,7 @@ import sys
 def main():
     rows = collections.defaultdict(lambda: collections.defaultdict(dict))
     for r in csv.DictReader(open(sys.argv[1])):
-        m = re.search(r"(exact_\w+|local_opt_exact\w*)", r.get("Kernel_Name", "")) if "Kernel_Name" in r else None
+        m = re.search(r"(exact_\w+|local_opt_exact\w*|score_\w+_kernel)", r.get("Kernel_Name", "")) if "Kernel_Name" in r else None
         name = m.group(1) if m else r.get("Kernel_Name", "kernel")[:40]
         key = (name, int(r["Grid_Size"]), int(r["Workgroup_Size"]))
         rows[key][int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
@@ -49,6 +49,9 @@ def main():
             h = sum(d["TCC_HIT_sum"] for d in ds)
             out["l2_hit_rate"] = h / max(h + sum(d["TCC_MISS_sum"] for d in ds), 1.0)
             out["l2_req_per_launch"] = (h + sum(d["TCC_MISS_sum"] for d in ds)) / len(ds)
+        for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+            if all(c in d for d in ds):   # per launch (FETCH / WRITE_SIZE in KB, x2 on gfx950 for bytes)
+                out[c] = sum(d[c] for d in ds) / len(ds)
         if all("SQ_WAVES" in d for d in ds):
             out["SQ_WAVES"] = sum(d["SQ_WAVES"] for d in ds) / len(ds)
         print(name, {k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.items()})

@@ -138,6 +138,8 @@ def main():
     text = f"""// GENERATED by tools/gen_refmath_tables.py -- do not edit.
 // Data of the libraries the reference's arithmetic runs in (glibc 2.35 libm,
 // numpy {numpy.__version__} SVML), for the bit-exact restatements in refmath.h.
+// Origins and licences: glibc's exp table (LGPL-2.1-or-later; exp by Arm),
+// Intel SVML's tables as bundled in numpy (BSD-3-Clause) -- THIRD_PARTY_NOTICES.md.
 #pragma once
 #include <stdint.h>
 

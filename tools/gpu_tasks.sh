@@ -226,7 +226,47 @@ for n in ${CHAINS:-1 16}; do
 done
 )
 
+# ---- cform: the exact local optima's c stored per optimum (exact_cform 0) against recomputed
+# from the parent's a rows (1), and the XCD-contiguous optimum order (exact_xcd): the bit-exact
+# GPU tests on the default, interleaved step A/Bs, then FETCH_SIZE / L2 / VALU / wait counters of
+# the local-optimum kernel at 16 chains for both forms (each counter set in its own pass)
+task_cform() (
+P=${PROF_DIR:-gpurun_out/cform}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$P/$name.log" 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -${TAILN:-4} "$P/$name.log"; return $rc; }
+if [ -z "$NO_TESTS" ]; then   # an assertion failure does not stop the A/B; a fault, abort or time limit does
+  TAILN=12 step tests 900 python -u -m pytest tests/test_gpu_exact.py tests/test_gpu_parity.py tests/test_gpu_rehearsal.py -q -rf -k "${TESTS:-exact or trajectory or raises or replica or rehearsal or ranks}" --timeout 300 --timeout-method thread; rc=$?
+  [ $rc -le 1 ] || exit $rc
+fi
+for n in ${CHAINS:-1 16 128}; do
+  TAILN=3 step ab_cform_$n 300 env AB_OPT=exact_cform AB_VALS=0,1 python tools/step_probe.py $n || exit 1
+done
+for n in ${XCD_CHAINS:-16 128}; do
+  TAILN=3 step ab_xcd_$n 300 env AB_OPT=exact_xcd AB_VALS=0,1 python tools/step_probe.py $n || exit 1
+done
+[ -n "$NO_PMC" ] && exit 0
+for f in 0 1; do
+  for cs in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+    tag=$(echo $cs | cut -d' ' -f1)
+    timeout -s KILL 180 env EXACT_CFORM=$f rocprofv3 --pmc $cs --kernel-include-regex "local_opt_exact" --output-format csv -d "$R/$P/pmc_${f}_$tag" -o p -- python "$R/tools/step_probe.py" 16 > "$P/pmc_${f}_$tag.log" 2>&1 || { echo "pmc $f $tag failed"; tail -3 "$P/pmc_${f}_$tag.log"; exit 1; }
+  done
+done
+echo "pmc done"
+)
+
+# ---- i8l_valu: SQ_INSTS_VALU of score_i8l_kernel (C3, B = 2048) for the default build and
+# the prep-only instrumented build (libnemo_abl32.so, NEMO_I8_ABLATE=32: no tiles walked), so
+# the walk's share is the difference (DESIGN.md 3.1h's per-cell accounting)
+task_i8l_valu() (
+P=${PROF_DIR:-gpurun_out/i8l_valu}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
+L=$R/nem-mcmc-optimization_amd/nemo
+for v in default abl32; do
+  lib=""; [ $v = abl32 ] && lib=$L/libnemo_abl32.so
+  timeout -s KILL 180 env NEMO_LIBRARY=$lib rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex "score_i8l" --output-format csv -d "$R/$P/$v" -o p -- python "$R/tools/i8l_probe.py" > "$P/$v.log" 2>&1 || { tail -3 "$P/$v.log"; exit 1; }
+  echo "== $v"; python tools/exact_pmc.py "$P/$v/p_counter_collection.csv"
+done
+)
+
 case "$task" in
-  ab|ab_step|batch|c4_rehearsal|exact|exact_ab|exact_dev|exact_pmc|exact_form|exact_prof|lo|prof|small|split|step_trace) "task_$task" "$@" ;;
-  *) echo "tasks: ab ab_step batch c4_rehearsal exact exact_ab exact_dev exact_pmc exact_form exact_prof lo prof small split step_trace"; exit 2 ;;
+  ab|ab_step|batch|c4_rehearsal|cform|i8l_valu|exact|exact_ab|exact_dev|exact_pmc|exact_form|exact_prof|lo|prof|small|split|step_trace) "task_$task" "$@" ;;
+  *) echo "tasks: ab ab_step batch c4_rehearsal cform i8l_valu exact exact_ab exact_dev exact_pmc exact_form exact_prof lo prof small split step_trace"; exit 2 ;;
 esac
