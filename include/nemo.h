@@ -156,6 +156,12 @@ int nemo_optimal_weights_end(nemo_ctx* ctx);
 /* order weights of chain `chain` from the last eval#1 of nemo_optimal_weights:
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);
+/* diagnostic (option "exact_trace" 1): the last exact fused step's local
+ * optima, [*n][4]: start / end times (wall_clock64, 100 MHz ticks) and the
+ * shader cycles spent in the objective / the optimiser's control, in launch
+ * order (chain-major, each chain's pair list); out may be NULL to query *n.
+ * No reference counterpart: profiling of the scheduling only. */
+int nemo_fetch_exact_trace(nemo_ctx* ctx, int* n, long long* out);
 
 /* ---- fixed-order optimizers of methods.py ---------
  * Every call handles nprob independent problems (one order each) with host

@@ -148,7 +148,8 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
                   c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf,
-                  c.d_xa,   c.d_xbits, c.d_pwpos};
+                  c.d_xa,   c.d_xbits, c.d_pwpos, c.d_xtrace, c.d_xqueue,
+                  c.d_xcost, c.d_xorder, c.d_xhist};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -341,6 +342,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
       HIPCHK(dalloc(&c.d_xhi, S));
       HIPCHK(dalloc(&c.d_pwplan, dev.size()));
       HIPCHK(dalloc(&c.d_pwpos, ppos.size()));
+      if (!c.d_xqueue) HIPCHK(dalloc(&c.d_xqueue, 1));
       HIPCHK(dalloc(&c.d_xbits, bits.size()));
       HIPCHK(hipMemcpy(c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
@@ -749,7 +751,23 @@ int exact_reserve(Ctx& c, int nchains) {
     ++c.graph_epoch;
     HIPCHK(hipStreamSynchronize(c.stream));
     HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
+    // the persistent form's schedule: each pair's last evaluation count (0:
+    // none yet) and the hand-out order
+    HIPCHK(dalloc(&c.d_xcost, nc * S * S));
+    HIPCHK(hipMemset(c.d_xcost, 0, nc * S * S * 4));
+    HIPCHK(dalloc(&c.d_xorder, nc * (size_t)nemo::pairs_per_chain(c.S, 0)));
+    HIPCHK(dalloc(&c.d_xhist, nc * 64));
+    c.cap_xorder = nc * (size_t)nemo::pairs_per_chain(c.S, 0);
     c.cap_xcells2 = nc;
+  }
+  if (c.exact_trace) {
+    const size_t need = nc * (size_t)nemo::pairs_per_chain(c.S, 0);
+    if (need > c.cap_xtrace) {
+      ++c.graph_epoch;
+      HIPCHK(hipStreamSynchronize(c.stream));
+      HIPCHK(dalloc(&c.d_xtrace, 4 * need));
+      c.cap_xtrace = need;
+    }
   }
   if (c.exact_cform == 1) {
     const size_t need = nc * S * plan;
@@ -1103,6 +1121,18 @@ int nemo_optimal_weights_end(nemo_ctx* ctx) {
   return j->rc;
 }
 
+int nemo_fetch_exact_trace(nemo_ctx* ctx, int* n, long long* out) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  if (!n) return fail(NEMO_ERR_ARG, "null n");
+  Ctx& c = ctx->c;
+  HIPCHK(hipStreamSynchronize(c.stream));
+  *n = c.xtrace_n;
+  if (out && c.xtrace_n > 0)
+    HIPCHK(hipMemcpy(out, c.d_xtrace, (size_t)c.xtrace_n * 4 * sizeof(long long), hipMemcpyDeviceToHost));
+  return NEMO_OK;
+}
+
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out) {
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
@@ -1278,6 +1308,18 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.exact_xcd = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "exact_sched") == 0) {
+    ctx->c.exact_sched = value ? 1 : 0;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "exact_persist") == 0) {
+    ctx->c.exact_persist = value ? 1 : 0;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "exact_trace") == 0) {
+    ctx->c.exact_trace = value ? 1 : 0;
+    return NEMO_OK;
+  }
   if (strcmp(name, "exact_lat_waves") == 0) {
     if (value < 0) return fail(NEMO_ERR_ARG, "exact_lat_waves %d", value);
     ctx->c.exact_lat_waves = value;
@@ -1348,6 +1390,9 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact_form") == 0) *value = c.exact_form;
   else if (strcmp(name, "exact_cform") == 0) *value = c.exact_cform;
   else if (strcmp(name, "exact_xcd") == 0) *value = c.exact_xcd;
+  else if (strcmp(name, "exact_trace") == 0) *value = c.exact_trace;
+  else if (strcmp(name, "exact_persist") == 0) *value = c.exact_persist;
+  else if (strcmp(name, "exact_sched") == 0) *value = c.exact_sched;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;

@@ -561,7 +561,24 @@ struct CArgs {
   const uint32_t* xbits = nullptr;   // kRc: [S][NS][64]
   double* cbuf = nullptr;            // stored: [optima][plan doubles]
   int xcd = 0;                       // XCD-contiguous optimum ranges (option exact_xcd)
+  long long* trace = nullptr;        // option exact_trace: [optima][4] start / end (wall_clock64), objective /
+                                     // control shader cycles
+  int* queue = nullptr;              // option exact_persist: the work counter (zeroed before the launch)
+  const int32_t* order = nullptr;    // the optima in the order they are handed out (null: launch order)
+  int32_t* cost = nullptr;           // option exact_sched: [chains][S][S] each pair's last evaluation count
 };
+
+// The persistent form (option exact_persist): resident blocks whose waves take
+// optima from a counter until none is left, so a wave's slot is refilled the
+// moment its optimum ends (in one-optimum-per-wave blocks a block's slots free
+// only when its slowest optimum ends: 0.56 of the slots busy on average at 16
+// C3 chains, tools/lo_timeline.py).  Every wave ends when the counter passes
+// the last optimum.  Lane 0 takes the item, the wave reads it uniformly.
+__device__ __forceinline__ int next_item(int* q, int lane) {
+  int v = 0;
+  if (lane == 0) v = atomicAdd(q, 1);
+  return __builtin_amdgcn_readfirstlane(v);
+}
 template <class Obj, int NS, bool kRc>
 __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E, int b, int k, size_t gw, double s,
                                         double lvlo, double lvhi, const double* __restrict__ owk,
@@ -628,10 +645,12 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   plan_to_lds<NS>(plan, nh, pl);
   __syncthreads();
   const int wv = threadIdx.x / kWave;
-  const int blk = xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks);
-  const int gw = __builtin_amdgcn_readfirstlane(blk * kExactWaves + wv);
   const int lane = threadIdx.x & (kWave - 1);
-  if (gw >= nchains * npairs) return;  // uniform per wave
+  const int total = nchains * npairs;
+  int item = ca.queue ? next_item(ca.queue, lane)
+                      : __builtin_amdgcn_readfirstlane(xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks) * kExactWaves + wv);
+  for (; item < total; item = ca.queue ? next_item(ca.queue, lane) : total) {   // uniform per wave
+  const int gw = ca.order ? __builtin_amdgcn_readfirstlane(ca.order[item]) : item;
   const int b = gw / npairs;
   const int n = gw - b * npairs;
   const int pk = pairs[(size_t)b * S * S + n];
@@ -640,6 +659,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
+  const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
   using Obj = ExactObjective<NS, true, kLat, false, kRc>;
   Obj obj;
   obj.tb = tabs.view();
@@ -652,11 +672,20 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
+  long long c_obj = 0, c_ctl = 0, tc = ca.trace ? (long long)clock64() : 0;   // (trace: shader cycles)
   while (lbx_run(st, lbx::Mem{mem[wv]})) {
     double f0, f1;
+    const long long t1 = ca.trace ? (long long)clock64() : 0;
     obj(st.x_eval, st.x1, f0, f1);
+    if (ca.trace) {
+      const long long t2 = (long long)clock64();
+      c_ctl += t1 - tc;
+      c_obj += t2 - t1;
+      tc = t2;
+    }
     lbx_feed(st, f0, f1);
   }
+  if (ca.trace) c_ctl += (long long)clock64() - tc;
   const LbfgsResult r{st.x, st.f, st.nit, st.nfev, st.status};
   if (lane == 0) {
     const double wx = refmath::expit(r.x, obj.tb);
@@ -667,6 +696,14 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
       const int nfev = r.nfev < 32767 ? r.nfev : 32767;
       info[idx] = (int32_t)(r.status | (nit << 4) | (nfev << 16));
     }
+    if (ca.cost) ca.cost[idx] = r.nfev;
+    if (ca.trace) {
+      ca.trace[4 * (size_t)gw] = t_start;
+      ca.trace[4 * (size_t)gw + 1] = (long long)wall_clock64();
+      ca.trace[4 * (size_t)gw + 2] = c_obj;
+      ca.trace[4 * (size_t)gw + 3] = c_ctl;
+    }
+  }
   }
 }
 
@@ -698,10 +735,23 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
     }
     return;
   }
+  __shared__ int s_item;
   tabs.fill(threadIdx.x, blockDim.x);
+  const int total = nchains * npairs;
+  // the optimum, uniform over the block: taken by thread 0 and handed to both
+  // waves through LDS (the barriers sit in straight-line code, executed the
+  // same number of times by both waves)
+  auto fetch = [&]() {
+    if (threadIdx.x == 0) s_item = atomicAdd(ca.queue, 1);
+    __syncthreads();
+    const int v = __builtin_amdgcn_readfirstlane(s_item);
+    __syncthreads();   // both waves hold it before thread 0 may take the next
+    return v;
+  };
   __syncthreads();
-  const int gw = xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks);   // the optimum: uniform over the block
-  if (gw >= nchains * npairs) return;
+  int item = ca.queue ? fetch() : xcd_block(ca.xcd, (int)blockIdx.x, lo_blocks);
+  while (item < total) {
+  const int gw = ca.order ? __builtin_amdgcn_readfirstlane(ca.order[item]) : item;
   const int b = gw / npairs;
   const int n = gw - b * npairs;
   const int pk = pairs[(size_t)b * S * S + n];
@@ -710,6 +760,7 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
   const size_t idx = ((size_t)b * S + i) * S + k;
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
+  const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
   // the throughput form's objective (few registers: four waves per SIMD
   // hold the 2 x 2016 waves of one chain's step), its plan in registers
   // (read once from global memory: no LDS copy, so eight blocks fit a CU)
@@ -729,11 +780,20 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
                         wv ? 0xaaaaaaaau : 0x55555555u);
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
+  long long c_obj = 0, c_ctl = 0, tc = ca.trace ? (long long)clock64() : 0;   // (trace: shader cycles)
   while (lbx_run(st, lbx::Mem{mem[wv]})) {
     double f0, f1;
+    const long long t1 = ca.trace ? (long long)clock64() : 0;
     obj(st.x_eval, st.x1, f0, f1);
+    if (ca.trace) {
+      const long long t2 = (long long)clock64();
+      c_ctl += t1 - tc;
+      c_obj += t2 - t1;
+      tc = t2;
+    }
     lbx_feed(st, f0, f1);
   }
+  if (ca.trace) c_ctl += (long long)clock64() - tc;
   if (wv == 0 && lane == 0) {
     const double wx = refmath::expit(st.x, obj.tb);
     wnew[idx] = wx;
@@ -743,6 +803,15 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
       const int nfev = st.nfev < 32767 ? st.nfev : 32767;
       info[idx] = (int32_t)(st.status | (nit << 4) | (nfev << 16));
     }
+    if (ca.cost) ca.cost[idx] = st.nfev;
+    if (ca.trace) {
+      ca.trace[4 * (size_t)gw] = t_start;
+      ca.trace[4 * (size_t)gw + 1] = (long long)wall_clock64();
+      ca.trace[4 * (size_t)gw + 2] = c_obj;
+      ca.trace[4 * (size_t)gw + 3] = c_ctl;
+    }
+  }
+  item = ca.queue ? fetch() : total;
   }
 }
 
@@ -817,6 +886,73 @@ __global__ void refmath_probe_kernel(int fn, int n, const double* __restrict__ x
     default: r = v; break;
   }
   out[g] = r;
+}
+
+// The hand-out order of the persistent form (option exact_sched 1): the
+// optima by their pair's evaluation count in the chain's previous step, most
+// first -- longest-processing-time first, so the long optimisations do not
+// start last and leave the end of the launch to a few waves
+// (tools/lo_timeline.py: at 16 C3 chains the last 27% of the launch ran below
+// half the resident waves).  Within one count the chains stay in launch order
+// (a chain's optima share the parent rows the recompute form reads, so the
+// waves in flight read few chains' rows at a time).  A counting sort in two
+// launches of one block per chain: the chain's histogram over kSchedBuckets
+// counts, then every block places its (count, chain) segment after all larger
+// counts and all earlier chains of its count.  The order within a segment is
+// whatever the LDS atomics give: it changes which wave takes which optimum,
+// never a bit.
+constexpr int kSchedBuckets = 64, kSchedThreads = 256;
+__device__ __forceinline__ int sched_bucket(const int32_t* __restrict__ pairs, const int32_t* __restrict__ cost,
+                                            int S, int b, int n) {
+  const int pk = pairs[(size_t)b * S * S + n];
+  const int c = cost[((size_t)b * S + (pk >> 16)) * S + (pk & 0xffff)] >> 1;   // evaluation pairs
+  return kSchedBuckets - 1 - (c < kSchedBuckets - 1 ? c : kSchedBuckets - 1);   // most work: bucket 0
+}
+
+__global__ __launch_bounds__(kSchedThreads) void exact_sched_hist_kernel(int S, int npairs,
+                                                                          const int32_t* __restrict__ pairs,
+                                                                          const int32_t* __restrict__ cost,
+                                                                          int* __restrict__ hist) {
+  __shared__ int h[kSchedBuckets];
+  const int b = blockIdx.x;
+  for (int q = threadIdx.x; q < kSchedBuckets; q += blockDim.x) h[q] = 0;
+  __syncthreads();
+  for (int n = threadIdx.x; n < npairs; n += blockDim.x) atomicAdd(&h[sched_bucket(pairs, cost, S, b, n)], 1);
+  __syncthreads();
+  for (int q = threadIdx.x; q < kSchedBuckets; q += blockDim.x) hist[(size_t)b * kSchedBuckets + q] = h[q];
+}
+
+__global__ __launch_bounds__(kSchedThreads) void exact_sched_place_kernel(int S, int npairs, int nchains,
+                                                                           const int32_t* __restrict__ pairs,
+                                                                           const int32_t* __restrict__ cost,
+                                                                           const int* __restrict__ hist,
+                                                                           int32_t* __restrict__ order) {
+  __shared__ int pos[kSchedBuckets];
+  __shared__ int col[kSchedBuckets];
+  const int b = blockIdx.x;
+  // segment (q, b) starts after every optimum of buckets < q and those of
+  // chains < b in bucket q: one thread per bucket sums its histogram column
+  for (int q = threadIdx.x; q < kSchedBuckets; q += blockDim.x) {
+    int tot = 0, before = 0;
+    for (int c = 0; c < nchains; ++c) {
+      const int v = hist[(size_t)c * kSchedBuckets + q];
+      tot += v;
+      before += c < b ? v : 0;
+    }
+    col[q] = tot;
+    pos[q] = before;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {   // the buckets before q (64 additions)
+    int acc = 0;
+    for (int q = 0; q < kSchedBuckets; ++q) {
+      pos[q] += acc;
+      acc += col[q];
+    }
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < npairs; n += blockDim.x)
+    order[atomicAdd(&pos[sched_bucket(pairs, cost, S, b, n)], 1)] = b * npairs + n;
 }
 
 }  // namespace
@@ -902,6 +1038,32 @@ struct LoArgs {
   SeqSumArgs fin;
 };
 
+// resident blocks of one kernel on the device at its block size (cached per kernel)
+template <auto K>
+int resident_blocks(int threads) {
+  static int n = -1;
+  if (n < 0) {
+    int per_cu = 0, dev = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, K, threads, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu < 1)
+      ncu = 256;
+    n = per_cu * ncu;
+  }
+  return n;
+}
+
+template <int NS, bool kRc>
+int lo_resident(int form) {
+  if (form == 3) return resident_blocks<local_opt_exact_pair_kernel<NS, kRc>>(2 * kWave);
+  if (form == 1) return resident_blocks<local_opt_exact_kernel<NS, true, kRc>>(kExactWaves * kWave);
+  return resident_blocks<local_opt_exact_kernel<NS, false, kRc>>(kExactWaves * kWave);
+}
+
+template <int NS>
+int lo_resident_ns(int form, bool rc) { return rc ? lo_resident<NS, true>(form) : lo_resident<NS, false>(form); }
+
 template <int NS, bool kRc>
 void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
   if (form == 3)
@@ -940,16 +1102,58 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   // form for few optima with two slots or more
   int form = c.exact_form;
   if (form == 0) form = nw <= c.exact_lat_waves ? 1 : 2;
-  if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves))) form = 3;
+  // (auto: the pair form up to 3 slots; from 4 its LDS and registers hold it
+  // to 1-2 waves per SIMD)
+  if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves && c.pw_ns <= 3)))
+    form = 3;
   if (c.pw_ns < 2 && form == 3) form = 2;
-  const int lo_blocks = form == 3 ? nw : (nw + kExactWaves - 1) / kExactWaves;
+  int lo_blocks = form == 3 ? nw : (nw + kExactWaves - 1) / kExactWaves;
+  // the persistent form: at most the resident blocks, the work counter zeroed
+  const bool persist = c.exact_persist && c.d_xqueue;
+  if (persist) {
+    int res = 0;
+    switch (c.pw_ns) {
+      case 1: res = lo_resident_ns<1>(form, rc); break;
+      case 2: res = lo_resident_ns<2>(form, rc); break;
+      case 3: res = lo_resident_ns<3>(form, rc); break;
+      case 4: res = lo_resident_ns<4>(form, rc); break;
+      case 5: res = lo_resident_ns<5>(form, rc); break;
+      case 6: res = lo_resident_ns<6>(form, rc); break;
+      case 7: res = lo_resident_ns<7>(form, rc); break;
+      case 8: res = lo_resident_ns<8>(form, rc); break;
+      default: return hipErrorInvalidValue;
+    }
+    lo_blocks = std::min(lo_blocks, std::max(res, 1));
+    const hipError_t me = hipMemsetAsync(c.d_xqueue, 0, sizeof(int), st);
+    if (me != hipSuccess) return me;
+  }
   const int per_fin = form == 3 ? 2 : kExactWaves;   // waves per appended block
   const int fin_blocks = d_ll1 ? (nchains + per_fin - 1) / per_fin : 0;
   LoArgs a{c.S,     c.E,      npairs,  nchains,  d_pairs,  d_w01,    d_anc,    d_ow,     c.d_xlo,
            c.d_xhi, c.d_D1w,  c.nwords, c.d_pwplan, c.pw_nh, c.pw_maxrem, sig0,  sig1,     d_wnew,
-           d_wdag,  d_info,   CArgs{c.d_xa, c.d_xbits, c.d_xcbuf, c.exact_xcd}, lo_blocks,
-           SeqSumArgs{d_cs1, c.E, nchains, d_ll1}};
+           d_wdag,  d_info,   CArgs{c.d_xa, c.d_xbits, c.d_xcbuf, c.exact_xcd,
+                                    c.exact_trace && c.cap_xtrace >= (size_t)nw ? c.d_xtrace : nullptr,
+                                    persist ? c.d_xqueue : nullptr, nullptr,
+                                    c.exact_sched && c.d_xcost ? c.d_xcost : nullptr},
+           lo_blocks, SeqSumArgs{d_cs1, c.E, nchains, d_ll1}};
+  // only when the optima outnumber the resident waves (else all start at once)
+  // and make at most 16 rounds of them: past that the last optimum's share of
+  // the launch is small and the chains' interleaving costs more (C3, 128
+  // chains: 11.99 against 11.84 ms per step, tools/step_probe.py)
+  const int per_block = form == 3 ? 1 : kExactWaves;   // optima a block holds at once
+  if (persist && c.exact_sched && c.d_xcost && c.d_xorder && c.cap_xorder >= (size_t)nw &&
+      nw > lo_blocks * per_block && nw <= 16 * lo_blocks * per_block) {
+    exact_sched_hist_kernel<<<nchains, kSchedThreads, 0, st>>>(c.S, npairs, d_pairs, c.d_xcost, c.d_xhist);
+    hipError_t se = hipGetLastError();
+    if (se != hipSuccess) return se;
+    exact_sched_place_kernel<<<nchains, kSchedThreads, 0, st>>>(c.S, npairs, nchains, d_pairs, c.d_xcost, c.d_xhist,
+                                                                c.d_xorder);
+    se = hipGetLastError();
+    if (se != hipSuccess) return se;
+    a.ca.order = c.d_xorder;
+  }
   const dim3 grid(lo_blocks + fin_blocks);
+  c.xtrace_n = a.ca.trace ? nw : 0;
   switch (c.pw_ns) {
     case 1: launch_lo_ns<1>(a, form, rc, grid, st); break;
     case 2: launch_lo_ns<2>(a, form, rc, grid, st); break;

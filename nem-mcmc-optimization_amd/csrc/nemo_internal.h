@@ -142,6 +142,22 @@ struct Ctx {
   size_t cap_xa = 0;               // its size in doubles
   uint32_t* d_xbits = nullptr;     // [S][pw_ns][64] lv bit of parent row k per (slot, lane): bit m, 16 = remainder
   int32_t* d_pwpos = nullptr;      // [E] plan position (u * 17 + m) * 64 + lane of element e
+  int exact_persist = 1;           // option "exact_persist": resident waves take optima from a counter
+  int* d_xqueue = nullptr;         // its counter (allocated at staging)
+  // option "exact_sched": 1 = hand the optima out longest-first by each pair's
+  // evaluation count in the chain's previous step (d_xcost [chains][S][S],
+  // written by the kernel; d_xorder [optima] built per launch)
+  int exact_sched = 1;
+  int32_t* d_xcost = nullptr;
+  int32_t* d_xorder = nullptr;
+  int* d_xhist = nullptr;          // [chains][64] the schedule's per-chain histograms
+  size_t cap_xorder = 0;           // optima d_xorder holds (d_xcost: cap_xcells2 chains)
+  // option "exact_trace" (diagnostic): each exact local optimum records its
+  // start and end time (wall_clock64, 100 MHz) into d_xtrace [optima][2]
+  int exact_trace = 0;
+  long long* d_xtrace = nullptr;
+  size_t cap_xtrace = 0;           // its optima
+  int xtrace_n = 0;                // optima the last traced launch recorded
 
   // worst-case |ll error| of the fixed-point kernels (nemo_host.h):
   // fx_colsum[k] = sum_e min(colbits_e, k) over the staged D1 bits; auto takes

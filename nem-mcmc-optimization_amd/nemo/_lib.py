@@ -56,6 +56,7 @@ SIGNATURES = [
                                               C.c_int, _vp, _vp, _vp, _vp]),
     ("nemo_optimal_weights_end", C.c_int, [_vp]),
     ("nemo_fetch_order_weights", C.c_int, [_vp, C.c_int, _f64p]),
+    ("nemo_fetch_exact_trace", C.c_int, [_vp, C.POINTER(C.c_int), C.c_void_p]),
     ("nemo_gamma_sweep", C.c_int, [_vp, C.c_int, _i32p, _f64p, C.c_int, _f64p, _f64p, _i32p]),
     ("nemo_inverse_ancestral", C.c_int, [_vp, C.c_int, _i32p, _f64p, _f64p]),
     ("nemo_inverse_sweep", C.c_int, [_vp, C.c_int, _i32p, _f64p, _f64p, _f64p, _i32p]),
