@@ -626,14 +626,20 @@ def main():
         pos_h = pos[:nch]
         w_h = rng.uniform(-3, 3, (nch, S, S))
         anc = np.clip(rng.random((nch, S, S)) - 0.5, 0, 1)
-        def fused_ms(nc, reps):
-            eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
-                                raise_on_fail=False)
+        def fused_ms(nc, reps, given_anc=False):
+            """one nemo_optimal_weights_w call (W in: W~ and ancestor_x made on
+            the device), or with given_anc the host's W~ / ancestor_x handed in"""
+            def call():
+                if given_anc:
+                    eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
+                                        raise_on_fail=False)
+                else:
+                    eng.optimal_weights_w(pos_h[:nc], w_h[:nc], SIG0, SIG1, cap=cap, raise_on_fail=False)
+            call()
             ts = []
             for _ in range(reps):
                 t0 = time.perf_counter()
-                eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
-                                    raise_on_fail=False)
+                call()
                 ts.append(time.perf_counter() - t0)
             return float(np.median(ts))
 
@@ -643,6 +649,7 @@ def main():
         # line-search path)
         exact_on = bool(eng.get_option("exact")) and bool(eng.get_option("exact_ok"))
         fs = fused_ms(nch, 5)
+        fs_given = fused_ms(nch, 5, given_anc=True)
         eng.set_option("exact", 0)
         fs_fast = fused_ms(nch, 5)
         fs1_fast = fused_ms(1, 20)
@@ -651,8 +658,11 @@ def main():
             "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
             "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
             "fast_kernels_ms_per_step": 1e3 * fs_fast,
-            "includes": "H2D of pos/W/anc, eval#1 with order weights, 2016 L-BFGS-B local optima "
-                        "per chain, eval#2 on binarised weights, D2H"}
+            "ms_per_step_given_ancestor": 1e3 * fs_given,
+            "includes": "nemo_optimal_weights_w: H2D of pos/W, W~ and ancestor_x (getrf/getri in scipy's bits) "
+                        "on the device, eval#1 with order weights, 2016 L-BFGS-B local optima per chain, eval#2 "
+                        "on binarised weights, D2H (ms_per_step_given_ancestor: the host's W~ / ancestor_x "
+                        "handed in instead)"}
         # BASELINE C3 names ONE chain: what one chain sees per call -- a
         # synchronous host-pointer order score (B = 1: the calculate_ll path of
         # one sampler, H2D + kernel + D2H) and the fused step of one chain
@@ -671,8 +681,7 @@ def main():
         ts1 = []
         for _ in range(20):
             t0 = time.perf_counter()
-            eng.optimal_weights(pos_h[:1], expit(w_h[:1]), anc[:1], w_h[:1], SIG0, SIG1, cap=cap,
-                                raise_on_fail=False)
+            eng.optimal_weights_w(pos_h[:1], w_h[:1], SIG0, SIG1, cap=cap, raise_on_fail=False)
             ts1.append(time.perf_counter() - t0)
         extras["single_chain"] = {
             "score_call_us": 1e6 * float(np.median(lat)), "evals_per_s_sequential": 1.0 / float(np.median(lat)),
@@ -682,8 +691,8 @@ def main():
             "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
             "reference_cpu_s_per_chain_step": 1.2,
             "includes": "score_call_us: one synchronous nemo_score call for one (pos, W) from host "
-                        "arrays; fused_step_ms: nemo_optimal_weights for one chain (eval#1 with order "
-                        "weights, 2016 local optima, eval#2, transfers)"}
+                        "arrays; fused_step_ms: nemo_optimal_weights_w for one chain (W~ and ancestor_x, "
+                        "eval#1 with order weights, 2016 local optima, eval#2, transfers)"}
         # the whole sampler: 16 chains' host state machines (reference call order,
         # Python random) + one fused device call per step
         from nemo import utils as nutils
@@ -691,13 +700,15 @@ def main():
         from nemo.invpool import InvPool, default_workers
         order0 = nutils.initial_order_guess(m.observed_knockdown_mat)
         seeds = [1234 + c for c in range(nch)]
-        nw = default_workers()  # up to 8 per rank: 0.59-0.66 ms per 16-chain step against 0.81-0.90 with 4 (tools/ab_workers.sh)
+        # ancestor_x on the device (the default at S <= 64); an InvPool of host
+        # worker processes (scipy's getrf / getri) beside it for the A/B
+        nw = default_workers()
         pool = InvPool(S, nch, n_workers=nw)
-        # the host side (worker processes, Python) is noisy run to run: three
-        # timed runs with the pool, the median reported
+        # the host side (Python) is noisy run to run: three timed runs, the
+        # median reported
         n_it = 30
         e2e = {}
-        for tag, pl, reps in (("pool", pool, 3), ("serial", None, 1)):
+        for tag, pl, reps in (("device", None, 3), ("pool", pool, 1)):
             ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pl).run(2)
             walls = []
             for _ in range(reps):
@@ -708,24 +719,26 @@ def main():
             e2e[tag] = (float(np.median(walls)), cb.best_scores, walls)
         # the same sampler with the fast kernels (the host's share of a step)
         eng.set_option("exact", 0)
-        ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pool).run(2)
-        cbf = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pool)
+        ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue").run(2)
+        cbf = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue")
         t0 = time.perf_counter()
         cbf.run(n_it)
         e2e_fast = time.perf_counter() - t0
         eng.set_option("exact", 1)
         pool.close()
-        dt = e2e["pool"][0]
+        dt = e2e["device"][0]
         extras["mcmc_end_to_end"] = {
             "chains": nch, "steps": n_it, "ms_per_step": 1e3 * dt / n_it,
-            "ms_per_step_runs": [1e3 * w / n_it for w in e2e["pool"][2]],
+            "ms_per_step_runs": [1e3 * w / n_it for w in e2e["device"][2]],
             "chain_steps_per_s": nch * n_it / dt,
-            "includes": f"ChainBatch.run: proposals, reset quirks, ancestor_x (scipy getrf/getri in {nw} "
-                        "InvPool worker processes) and accept per chain on the host + the fused device step",
-            "ms_per_step_serial_inv": 1e3 * e2e["serial"][0] / n_it,
+            "over_fused_step": (dt / n_it) / fs,
+            "includes": "ChainBatch.run: proposals, reset quirks and accept per chain on the host + the fused "
+                        "device step from W (W~ and ancestor_x on the device, in scipy's bits)",
+            "ms_per_step_host_pool": 1e3 * e2e["pool"][0] / n_it,
+            "host_pool_workers": nw,
             "arithmetic": "exact (the reference's bits)" if exact_on else "fast",
             "ms_per_step_fast_kernels": 1e3 * e2e_fast / n_it,
-            "pool_bits_equal_serial": bool(np.array_equal(e2e["pool"][1], e2e["serial"][1])),
+            "device_bits_equal_host_pool": bool(np.array_equal(e2e["device"][1], e2e["pool"][1])),
             "reference_cpu_s_per_chain_step": 1.2}
         if args.config == "C3":
             # BASELINE config C5 (128 x 5000, parent cap 6): the capped

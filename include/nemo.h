@@ -47,7 +47,8 @@ enum {
   NEMO_ERR_ARG = -1,     /* bad argument (shape, pointer, range)          */
   NEMO_ERR_HIP = -2,     /* HIP runtime error (no device, OOM, launch)    */
   NEMO_ERR_STATE = -3,   /* tables not staged / capacity not reserved     */
-  NEMO_ERR_OPT = -5      /* a local optimisation did not converge         */
+  NEMO_ERR_OPT = -5,     /* a local optimisation did not converge         */
+  NEMO_ERR_LINALG = -6   /* ancestor_x: I - W~ singular or not finite      */
 };
 
 /* per-problem termination codes of the local optimiser (scipy task names) */
@@ -153,6 +154,31 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
                                const double* anc, double sig0, double sig1, int cap, double* w_new,
                                double* ll1, double* ll_dag, int32_t* info);
 int nemo_optimal_weights_end(nemo_ctx* ctx);
+/* nemo_optimal_weights from the weights themselves, as the reference's step
+ * starts (nem_order_mcmc.py:172-208 with :98-103 and :185): the device makes
+ * each chain's W~ = expit(W) on the permissible entries (cap as below; the
+ * other entries W's own) and ancestor_x = clip(inv(I - W~) - I, 0, 1) in
+ * scipy.linalg.inv's bits (LAPACK getrf + getri of scipy's OpenBLAS 0.3.28,
+ * restated in csrc/nemo_ancestor.hip), then runs the step on them.  S <= 64.
+ *   w        [nchains][S][S]  the weights W (after the proposal's reset)
+ *   w01_out, anc_out [nchains][S][S]  nullable: W~ and ancestor_x
+ *   anc_flag [nchains]        nullable: 0, or 1 singular / 2 not finite /
+ *                             4 non-finite factors (recompute on the host)
+ * Returns NEMO_ERR_LINALG when a flag is set (the step's results are then
+ * not meaningful: scipy.linalg.inv raises LinAlgError / ValueError for 1 / 2),
+ * else as nemo_optimal_weights.  _begin: the queued form (ended by
+ * nemo_optimal_weights_end, in submission order with the other _begin). */
+int nemo_optimal_weights_w(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w, double sig0,
+                           double sig1, int cap, double* w01_out, double* anc_out, double* w_new,
+                           double* ll1, double* ll_dag, int32_t* info, int32_t* anc_flag);
+int nemo_optimal_weights_w_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w,
+                                 double sig0, double sig1, int cap, double* w01_out, double* anc_out,
+                                 double* w_new, double* ll1, double* ll_dag, int32_t* info,
+                                 int32_t* anc_flag);
+/* the same W~ / ancestor_x / flags on device buffers, queued on `stream`
+ * (null: HIP's null stream); feeds nemo_optimal_weights_dev.  S <= 64. */
+int nemo_ancestor_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w, int cap,
+                      double* d_w01, double* d_anc, int32_t* d_flag, void* stream);
 /* order weights of chain `chain` from the last eval#1 of nemo_optimal_weights:
  * (S+1)*E doubles (NEMOrderMCMC.order_weights after get_optimal_weights) */
 int nemo_fetch_order_weights(nemo_ctx* ctx, int chain, double* ow_out);

@@ -25,6 +25,10 @@ struct StepJob {
   double sig0, sig1;
   double *w_new, *ll1, *ll_dag;
   int32_t* info;
+  // nemo_optimal_weights_w_begin: W in, W~ / ancestor_x / flags out
+  const double* w_in = nullptr;
+  double *w01_out = nullptr, *anc_out = nullptr;
+  int32_t* aflag = nullptr;
   int rc = 0;
   std::string err;
   int slot = 0;  // staging slot while in flight
@@ -891,24 +895,29 @@ int nemo_optimal_weights_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, c
 
 namespace {
 
-// every transfer of a fused step goes through a pinned staging slot: [pos |
-// w01 | anc | w_new | info | ll1 | ll_dag | eval #2's partials], each part
-// 256-B aligned, and a device block with the same layout: one H2D of [pos ..
-// anc], info preset to -1 (= not a permissible pair) by the step's prep, one
-// D2H of [w_new .. partials]; the host hands back w_new at the entries info
-// marks (the caller's values stay everywhere else) and sums eval #2's
-// partials (npart: the most any score kernel writes per evaluation)
+// every transfer of a fused step goes through a pinned staging slot: [W |
+// pos | w01 | anc | w_new | info | ll1 | ll_dag | ancestor flags | eval #2's
+// partials], each part 256-B aligned, and a device block with the same
+// layout.  Given W~ and ancestor_x (nemo_optimal_weights): one H2D of [pos ..
+// anc], one D2H of [w_new .. partials].  Given W (nemo_optimal_weights_w):
+// one H2D of [W | pos], the device computes W~ and ancestor_x in place, one
+// D2H of [w01 .. partials].  info is preset to -1 (= not a permissible pair)
+// by the step's prep; the host hands back w_new at the entries info marks
+// (the caller's values stay everywhere else) and sums eval #2's partials
+// (npart: the most any score kernel writes per evaluation)
 struct StepLayout {
-  size_t o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, o_part, total;
+  size_t o_pos, o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, o_flag, o_part, total;
   StepLayout(size_t S, size_t n, size_t npart) {
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    o_w01 = up(n * S * 4);
+    o_pos = up(n * S * S * 8);
+    o_w01 = o_pos + up(n * S * 4);
     o_anc = o_w01 + up(n * S * S * 8);
     o_wn = o_anc + up(n * S * S * 8);
     o_inf = o_wn + up(n * S * S * 8);
     o_ll1 = o_inf + up(n * S * S * 4);
     o_lld = o_ll1 + up(n * 8);
-    o_part = o_lld + up(n * 8);
+    o_flag = o_lld + up(n * 8);
+    o_part = o_flag + up(n * 4);
     total = o_part + up(n * npart * 8);
   }
 };
@@ -923,13 +932,17 @@ extern "C" {
 // queue the device work (one H2D copy, the launches, one D2H copy) and record
 // the slot's event; returns without waiting
 static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, const double* w01,
-                      const double* anc, double sig0, double sig1, int cap, const double* w_new) {
+                      const double* anc, const double* w_in, double sig0, double sig1, int cap,
+                      const double* w_new) {
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
   if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
   if (nchains == 0) return NEMO_OK;
-  if (!pos || !w01 || !anc || !w_new) return fail(NEMO_ERR_ARG, "null host pointer");
+  const bool from_w = w_in != nullptr;
+  if (!pos || (!from_w && (!w01 || !anc)) || !w_new) return fail(NEMO_ERR_ARG, "null host pointer");
   Ctx& c = ctx->c;
+  if (from_w && !nemo::ancestor_supported(c))
+    return fail(NEMO_ERR_ARG, "S=%d > 64: ancestor_x on the device covers S <= 64 (give W~ and ancestor_x)", c.S);
   if ((rc = check_pos(pos, nchains, c.S))) return rc;
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
   if (cap >= 0 && step_exact(c, cap) && (rc = exact_reserve(c, nchains))) return rc;
@@ -939,22 +952,34 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if ((rc = step_stage(c, slot, L.total))) return rc;
   char* hs = (char*)c.h_stage[slot];
   char* ds = (char*)c.d_step[slot];
-  memcpy(hs, pos, n * S * 4);
-  memcpy(hs + L.o_w01, w01, n * S * S * 8);
-  memcpy(hs + L.o_anc, anc, n * S * S * 8);
+  memcpy(hs + L.o_pos, pos, n * S * 4);
+  if (from_w) {
+    memcpy(hs, w_in, n * S * S * 8);
+  } else {
+    memcpy(hs + L.o_w01, w01, n * S * S * 8);
+    memcpy(hs + L.o_anc, anc, n * S * S * 8);
+  }
   // replayed as a hipGraph per (nchains, cap, slot) while no captured
   // argument changes (the staging buffers, options and tables bump
   // graph_epoch), so a step costs one graph launch instead of ~10 API calls
   int np2 = 0;
   auto enqueue = [&]() -> int {
-    HIPCHK(hipMemcpyAsync(ds, hs, L.o_wn, hipMemcpyHostToDevice, st));  // info: preset by the prep
-    int r = optimal_weights_enqueue(ctx, nchains, (const int32_t*)ds, (const double*)(ds + L.o_w01),
+    const int32_t* d_pos = (const int32_t*)(ds + L.o_pos);
+    if (from_w) {  // [W | pos] in; W~ and ancestor_x made in place
+      HIPCHK(hipMemcpyAsync(ds, hs, L.o_w01, hipMemcpyHostToDevice, st));
+      HIPCHK(nemo::launch_ancestor(c, nchains, cap, d_pos, (const double*)ds, (double*)(ds + L.o_w01),
+                                   (double*)(ds + L.o_anc), (int32_t*)(ds + L.o_flag), st));
+    } else {  // info: preset by the prep
+      HIPCHK(hipMemcpyAsync(ds + L.o_pos, hs + L.o_pos, L.o_wn - L.o_pos, hipMemcpyHostToDevice, st));
+    }
+    int r = optimal_weights_enqueue(ctx, nchains, d_pos, (const double*)(ds + L.o_w01),
                                     (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
                                     (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st,
                                     c.step_host_sum && L.o_part < L.total ? (double*)(ds + L.o_part) : nullptr,
                                     &np2);
     if (r) return r;  // np2 <= step_npart: checked by launch_score_factored before it launched
-    HIPCHK(hipMemcpyAsync(hs + L.o_wn, ds + L.o_wn, L.total - L.o_wn, hipMemcpyDeviceToHost, st));
+    const size_t o_out = from_w ? L.o_w01 : L.o_wn;
+    HIPCHK(hipMemcpyAsync(hs + o_out, ds + o_out, L.total - o_out, hipMemcpyDeviceToHost, st));
     return NEMO_OK;
   };
   Ctx::StepGraph* sg = nullptr;
@@ -962,7 +987,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if (c.graphs && !c.timing) {
     for (auto& g : c.step_graph)
       if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.slot == slot &&
-          g.sig0 == sig0 && g.sig1 == sig1)
+          g.sig0 == sig0 && g.sig1 == sig1 && g.from_w == from_w)
         sg = &g;
     if (!sg) {  // capture once
       Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
@@ -992,6 +1017,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
           g.slot = slot;
           g.sig0 = sig0;
           g.sig1 = sig1;
+          g.from_w = from_w;
           g.epoch = c.graph_epoch;
           g.np2 = np2;
           sg = &g;
@@ -1024,13 +1050,25 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
 // second half: wait for the slot's device work, hand the outputs back and
 // raise the reference's error for a failed local optimisation
 static int step_finish(nemo_ctx* ctx, int slot, int nchains, double* w_new, double* ll1, double* ll_dag,
-                       int32_t* info) {
+                       int32_t* info, bool from_w = false, double* w01_out = nullptr, double* anc_out = nullptr,
+                       int32_t* aflag = nullptr) {
   Ctx& c = ctx->c;
   if (nchains == 0) return NEMO_OK;
   const size_t S = c.S, n = nchains;
   const StepLayout L(S, n, step_npart(c));
   HIPCHK(hipEventSynchronize(c.step_done[slot]));
   const char* hs = (const char*)c.h_stage[slot];
+  if (from_w) {
+    if (w01_out) memcpy(w01_out, hs + L.o_w01, n * S * S * 8);
+    if (anc_out) memcpy(anc_out, hs + L.o_anc, n * S * S * 8);
+    const int32_t* fl = (const int32_t*)(hs + L.o_flag);
+    if (aflag) memcpy(aflag, fl, n * 4);
+    for (size_t b = 0; b < n; ++b)
+      if (fl[b])
+        return fail(NEMO_ERR_LINALG, "ancestor_x of chain %zu: %s", b,
+                    (fl[b] & 2) ? "I - W~ is not finite" : (fl[b] & 1) ? "singular matrix"
+                                                                      : "non-finite factors (recompute on the host)");
+  }
   memcpy(ll1, hs + L.o_ll1, n * 8);
   if (const int np2 = c.step_np2[slot]) {  // eval #2's partials: the device's fixed-order sum, on the host
     const double* part = (const double*)(hs + L.o_part);
@@ -1064,9 +1102,18 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
                          const double* anc, double sig0, double sig1, int cap, double* w_new,
                          double* ll1, double* ll_dag, int32_t* info) {
   if (!ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
-  int rc = step_start(ctx, 0, nchains, pos, w01, anc, sig0, sig1, cap, w_new);
+  int rc = step_start(ctx, 0, nchains, pos, w01, anc, nullptr, sig0, sig1, cap, w_new);
   if (rc) return rc;
   return step_finish(ctx, 0, nchains, w_new, ll1, ll_dag, info);
+}
+
+int nemo_optimal_weights_w(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w, double sig0,
+                           double sig1, int cap, double* w01_out, double* anc_out, double* w_new, double* ll1,
+                           double* ll_dag, int32_t* info, int32_t* anc_flag) {
+  if (!ll1 || !ll_dag || !w) return fail(NEMO_ERR_ARG, "null host pointer");
+  int rc = step_start(ctx, 0, nchains, pos, nullptr, nullptr, w, sig0, sig1, cap, w_new);
+  if (rc) return rc;
+  return step_finish(ctx, 0, nchains, w_new, ll1, ll_dag, info, true, w01_out, anc_out, anc_flag);
 }
 
 // asynchronous form: the library thread runs each call's transfers, launches
@@ -1074,6 +1121,8 @@ int nemo_optimal_weights(nemo_ctx* ctx, int nchains, const int32_t* pos, const d
 // are in flight at once (staging slots 1 and 2): the thread stages and queues
 // the next call while the device still runs the previous one, then waits for
 // that one (nemo_host.h StepQueue)
+static int steps_submit(nemo_ctx* ctx, std::unique_ptr<StepJob> j);
+
 int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w01,
                                const double* anc, double sig0, double sig1, int cap, double* w_new,
                                double* ll1, double* ll_dag, int32_t* info) {
@@ -1081,6 +1130,27 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
   if (rc) return rc;
   if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
   if (!pos || !w01 || !anc || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  return steps_submit(
+      ctx, std::unique_ptr<StepJob>(new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info}));
+}
+
+int nemo_optimal_weights_w_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, const double* w, double sig0,
+                                 double sig1, int cap, double* w01_out, double* anc_out, double* w_new,
+                                 double* ll1, double* ll_dag, int32_t* info, int32_t* anc_flag) {
+  int rc = check_ctx(ctx, true);
+  if (rc) return rc;
+  if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
+  if (!pos || !w || !w_new || !ll1 || !ll_dag) return fail(NEMO_ERR_ARG, "null host pointer");
+  std::unique_ptr<StepJob> j(
+      new StepJob{nchains, cap, pos, nullptr, nullptr, sig0, sig1, w_new, ll1, ll_dag, info});
+  j->w_in = w;
+  j->w01_out = w01_out;
+  j->anc_out = anc_out;
+  j->aflag = anc_flag;
+  return steps_submit(ctx, std::move(j));
+}
+
+static int steps_submit(nemo_ctx* ctx, std::unique_ptr<StepJob> j) {
   std::string err;
   try {
     if (!ctx->steps) {
@@ -1088,7 +1158,8 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
       ctx->steps.reset(new nemo::host::StepQueue<StepJob>(
           [ctx, next_slot](StepJob& j) {  // start: true = in flight
             j.slot = *next_slot;
-            j.rc = step_start(ctx, j.slot, j.nchains, j.pos, j.w01, j.anc, j.sig0, j.sig1, j.cap, j.w_new);
+            j.rc = step_start(ctx, j.slot, j.nchains, j.pos, j.w01, j.anc, j.w_in, j.sig0, j.sig1, j.cap,
+                              j.w_new);
             if (j.rc) {
               j.err = g_err;
               (void)hipStreamSynchronize(ctx->c.stream);  // nothing of it left running in its slot
@@ -1100,12 +1171,12 @@ int nemo_optimal_weights_begin(nemo_ctx* ctx, int nchains, const int32_t* pos, c
           },
           [ctx](StepJob& j) { return hipEventQuery(ctx->c.step_done[j.slot]) != hipErrorNotReady; },
           [ctx](StepJob& j) {
-            j.rc = step_finish(ctx, j.slot, j.nchains, j.w_new, j.ll1, j.ll_dag, j.info);
+            j.rc = step_finish(ctx, j.slot, j.nchains, j.w_new, j.ll1, j.ll_dag, j.info, j.w_in != nullptr,
+                               j.w01_out, j.anc_out, j.aflag);
             if (j.rc) j.err = g_err;
           },
           2));
     }
-    std::unique_ptr<StepJob> j(new StepJob{nchains, cap, pos, w01, anc, sig0, sig1, w_new, ll1, ll_dag, info});
     if (ctx->steps->submit(std::move(j), &err)) return NEMO_OK;
   } catch (const std::exception& e) {
     err = e.what();
@@ -1119,6 +1190,19 @@ int nemo_optimal_weights_end(nemo_ctx* ctx) {
   if (!j) return fail(NEMO_ERR_STATE, "no nemo_optimal_weights_begin to end");
   if (j->rc) g_err = j->err;
   return j->rc;
+}
+
+int nemo_ancestor_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w, int cap,
+                      double* d_w01, double* d_anc, int32_t* d_flag, void* stream) {
+  int rc = check_ctx(ctx, false);
+  if (rc) return rc;
+  Ctx& c = ctx->c;
+  if (nchains < 0 || cap < 0) return fail(NEMO_ERR_ARG, "nchains=%d cap=%d", nchains, cap);
+  if (!nemo::ancestor_supported(c)) return fail(NEMO_ERR_ARG, "S=%d > 64", c.S);
+  if (nchains == 0) return NEMO_OK;
+  if (!d_pos || !d_w || !d_w01 || !d_anc || !d_flag) return fail(NEMO_ERR_ARG, "null device pointer");
+  HIPCHK(nemo::launch_ancestor(c, nchains, cap, d_pos, d_w, d_w01, d_anc, d_flag, pick(ctx, stream)));
+  return NEMO_OK;
 }
 
 int nemo_fetch_exact_trace(nemo_ctx* ctx, int* n, long long* out) {

@@ -198,6 +198,7 @@ struct Ctx {
     int nchains = -1, cap = -1, slot = -1;
     int np2 = 0;                   // eval #2's partials per chain left for the host (0: ll_dag on device)
     double sig0 = 0.0, sig1 = 0.0;
+    bool from_w = false;           // nemo_optimal_weights_w: ancestor_x made on the device
     uint64_t epoch = 0;
     hipGraphExec_t exec = nullptr;
   };
@@ -520,5 +521,12 @@ hipError_t launch_step_prep(Ctx& c, int batch, int cap, const int32_t* d_pos, co
 // resolves to for this cap / output set), with the worst-case |ll error| of
 // its fixed-point arithmetic (0 for the fp64 kernels); -1 if none applies
 int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound);
+// the step's W~ and ancestor_x from W on the device, in scipy's bits
+// (nemo_ancestor.hip; S <= 64): d_w01 = expit on the permissible entries (cap
+// as for the step), d_anc = clip(inv(I - W~) - I, 0, 1), d_flag [nchains]: 1
+// singular, 2 non-finite I - W~, 4 non-finite factors (the host recomputes)
+bool ancestor_supported(const Ctx& c);
+hipError_t launch_ancestor(Ctx& c, int nchains, int cap, const int32_t* d_pos, const double* d_w, double* d_w01,
+                           double* d_anc, int32_t* d_flag, hipStream_t st);
 
 }  // namespace nemo

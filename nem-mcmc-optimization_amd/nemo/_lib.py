@@ -21,7 +21,7 @@ _PATH = os.environ.get("NEMO_LIBRARY") or os.path.join(os.path.dirname(os.path.a
                                                        "libnemo.so")
 
 NEMO_F64, NEMO_F32 = 0, 1
-NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT = 0, -1, -2, -3, -5
+NEMO_OK, NEMO_ERR_ARG, NEMO_ERR_HIP, NEMO_ERR_STATE, NEMO_ERR_OPT, NEMO_ERR_LINALG = 0, -1, -2, -3, -5, -6
 # per-pair L-BFGS-B status in the low 4 bits of ``info`` (include/nemo.h)
 LBFGSB_CONV_PGTOL, LBFGSB_CONV_REL, LBFGSB_ABNORMAL, LBFGSB_MAXITER = 0, 1, 2, 3
 
@@ -55,6 +55,11 @@ SIGNATURES = [
     ("nemo_optimal_weights_begin", C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, C.c_double,
                                               C.c_int, _vp, _vp, _vp, _vp]),
     ("nemo_optimal_weights_end", C.c_int, [_vp]),
+    ("nemo_optimal_weights_w", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_double, C.c_double, C.c_int,
+                                          _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nemo_optimal_weights_w_begin", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_double, C.c_double, C.c_int,
+                                                _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("nemo_ancestor_dev", C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int, _vp, _vp, _vp, _vp]),
     ("nemo_fetch_order_weights", C.c_int, [_vp, C.c_int, _f64p]),
     ("nemo_fetch_exact_trace", C.c_int, [_vp, C.POINTER(C.c_int), C.c_void_p]),
     ("nemo_gamma_sweep", C.c_int, [_vp, C.c_int, _i32p, _f64p, C.c_int, _f64p, _f64p, _i32p]),

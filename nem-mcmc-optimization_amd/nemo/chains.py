@@ -154,12 +154,46 @@ def _finish(chains, engine: Engine, prep, res, use_nem, cap):
     return out
 
 
+def _device_ancestor(engine: Engine, pool) -> bool:
+    """W~ and ancestor_x made on the device (nemo_optimal_weights_w, S <= 64)
+    unless an ``InvPool`` is given: then the host makes them in its workers."""
+    return pool is None and engine.device_ancestor
+
+
+def _w_call_end(chains, call, raise_on_fail, drain=None):
+    """The result of an ended ``nemo_optimal_weights_w`` call and the prep tuple
+    ``_finish`` takes; sets every chain's ancestor_x.  A non-finite value inside
+    the device's factorisation (never met on the sampler's matrices) reruns the
+    step with the host's ancestor_x, after ``drain()`` has ended every call
+    queued behind it."""
+    from .engine import AncestorRecompute
+    try:
+        res = call.result(raise_on_fail)
+    except AncestorRecompute:
+        if drain is not None:
+            drain()
+        call.recompute()
+        res = call.result(raise_on_fail)
+    for k, c in enumerate(chains):
+        c.ll = 0.0
+        c.ancestor_x = call.anc[k]
+    return (call.pos, call.w, call.w01, call.anc), res
+
+
 def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on_fail=True, pool=None):
     """``get_optimal_weights(init=True)`` (nem_order_mcmc.py:172-208) of every
     chain in ONE fused device call; each chain's state is updated exactly as
     its own call would (same kernels, batch-invariant bits).  A failed local
     optimisation raises the reference's Exception (nem_order_mcmc.py:168-169);
-    with ``raise_on_fail=False`` the step keeps the optimiser's last point."""
+    with ``raise_on_fail=False`` the step keeps the optimiser's last point.
+    W~ and ancestor_x come from the device (S <= 64, no ``pool``) or the host."""
+    if _device_ancestor(engine, pool):
+        pos = np.stack([c._pos for c in chains]).astype(np.int32)
+        w = np.stack([c.parent_weights for c in chains])
+        call = engine.bind_optimal_weights_w(pos, w, SIG0, SIG1, cap=cap)
+        call.run()
+        prep, res = _w_call_end(chains, call, raise_on_fail)
+        return _finish(chains, engine, prep, res, use_nem, cap)
     prep = _prepare(chains, pool)
     return _finish(chains, engine, prep, _device_step(engine, prep, cap, raise_on_fail), use_nem, cap)
 
@@ -189,7 +223,8 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     ``raise_on_fail`` is set, the reference's Exception propagates and the
     chains' states are unspecified afterwards (see the pipeline below).
     ``pool`` (an ``InvPool``) runs the ancestor_x inversions in worker
-    processes; the results do not change.  ``groups``: the number of chain
+    processes instead of the device (which makes them at S <= 64); the results
+    do not change.  ``groups``: the number of chain
     groups in the pipeline below (default 3 from 6 chains, else 2)."""
     n = len(chains)
     s = chains[0].num_s
@@ -239,10 +274,10 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                     q["best_order_list"].append(q["best_order"])
 
     # Chain groups in a software pipeline: the device step of a group runs on
-    # the library's step thread (nemo_optimal_weights_begin / _end) while the
-    # host accepts / proposes / resets the others.  Per group: propose, hand
-    # its ancestor_x to the pool's workers, finish the oldest running group
-    # (its accept) while they compute, then queue this group's step.  With
+    # the library's step thread (nemo_optimal_weights[_w]_begin / _end) while
+    # the host accepts / proposes / resets the others.  Per group: propose,
+    # (host ancestor_x only: hand it to the pool's workers, finish the oldest
+    # running group while they compute,) then queue this group's step.  With
     # three or more groups one more step stays queued on the device while the
     # host does that, so the device goes from group to group without waiting
     # for the host; with two, the step is queued before the other one is
@@ -268,11 +303,19 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         pending = deque()
         wst = [None] * n_groups     # each group's weights stack (its last step's w_new)
         early = n_groups >= 3       # finish the oldest group before queuing the next
+        dev = _device_ancestor(engine, pool)
+
+        def drain():
+            for p in pending:
+                p[3].end()
 
         def collect():
             g, cs, prep, call = pending.popleft()
             call.end()
-            res = call.result(raise_on_fail)
+            if dev:
+                prep, res = _w_call_end(cs, call, raise_on_fail, drain)
+            else:
+                res = call.result(raise_on_fail)
             wst[g] = res[0]
             post(glist[g], _finish(cs, engine, prep, res, False, cap))
 
@@ -282,12 +325,19 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                     stacks = propose(idx, wst[g])
                     wst[g] = None
                     cs = [chains[k] for k in idx]
-                    part = _prepare_start(cs, pool, stacks)
-                    while early and len(pending) > n_groups - 2:
-                        collect()
-                    prep = _prepare_end(cs, part, pool)
-                    pos, w, w01, anc = prep
-                    call = engine.bind_optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
+                    if dev:
+                        while early and len(pending) > n_groups - 2:
+                            collect()
+                        prep = None
+                        call = engine.bind_optimal_weights_w(stacks[0].astype(np.int32), stacks[1], SIG0, SIG1,
+                                                             cap=cap)
+                    else:
+                        part = _prepare_start(cs, pool, stacks)
+                        while early and len(pending) > n_groups - 2:
+                            collect()
+                        prep = _prepare_end(cs, part, pool)
+                        pos, w, w01, anc = prep
+                        call = engine.bind_optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap)
                     call.begin()
                     pending.append((g, cs, prep, call))
                     while len(pending) > n_groups - 1:
@@ -507,7 +557,8 @@ def run_c4(nem, engine: Engine, n_chains: int = 128, steps: int = 10, warmup_ste
     mine = shard(n_chains, rank, world)
     order = utils.initial_order_guess(nem.observed_knockdown_mat)
     seeds = [1234 + c for c in mine]
-    nw = default_workers() if inv_workers is None else int(inv_workers)
+    # ancestor_x: on the device at S <= 64 (no worker processes), else in an InvPool
+    nw = (0 if engine.device_ancestor else default_workers()) if inv_workers is None else int(inv_workers)
     pool = InvPool(nem.num_s, len(mine), nw) if nw > 0 and len(mine) > 0 else None
     try:
         if warmup_steps > 0 and len(mine):

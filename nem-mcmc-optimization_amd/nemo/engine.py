@@ -175,6 +175,30 @@ class Engine:
         returns."""
         return _OptimalWeightsCall(self, pos, w01, anc, w_prev, sig0, sig1, cap)
 
+    @property
+    def device_ancestor(self) -> bool:
+        """True when the fused step can start from W itself: W~ and
+        ancestor_x made on the device in scipy's bits (S <= 64)."""
+        return self.S <= 64
+
+    def optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0, raise_on_fail=True):
+        """``optimal_weights`` from the weights themselves: the device makes
+        W~ and ancestor_x (nem_order_mcmc.py:98-103, :185) as scipy does.
+        Returns (w01, anc, w_new, ll1, ll_dag, info)."""
+        call = self.bind_optimal_weights_w(pos, w, sig0, sig1, cap=cap)
+        call.run()
+        try:
+            res = call.result(raise_on_fail)
+        except AncestorRecompute:
+            call.recompute()
+            res = call.result(raise_on_fail)
+        return (call.w01, call.anc) + res
+
+    def bind_optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0):
+        """``optimal_weights_w`` in parts, as ``bind_optimal_weights``; the
+        call's ``w01`` / ``anc`` hold W~ and ancestor_x once it has ended."""
+        return _OptimalWeightsWCall(self, pos, w, sig0, sig1, cap)
+
     # -- fixed-order optimizers (methods.py) --------------------------------
     def _sweep(self, fn, pos, w, *extra, raise_on_fail=True):
         pos = i32(np.atleast_2d(pos))
@@ -352,6 +376,81 @@ class _OptimalWeightsCall:
             return self.w_new, self.ll1, self.lld, self.info
         if rc == _lib.NEMO_ERR_OPT:
             # the reference raises a plain Exception (nem_order_mcmc.py:168-169)
+            raise Exception(_lib.load().nemo_last_error().decode())
+        check(rc)
+        return self.w_new, self.ll1, self.lld, self.info
+
+
+class AncestorRecompute(_lib.NemoError):
+    """The device's ancestor_x met a non-finite intermediate value, where its
+    restatement is not held to scipy's bits: the step is to be recomputed with
+    the host's W~ / ancestor_x (``_OptimalWeightsWCall.recompute``)."""
+
+
+class _OptimalWeightsWCall:
+    """``nemo_optimal_weights_w``: W in; W~, ancestor_x and the step out."""
+    __slots__ = ("eng", "pos", "w", "w01", "anc", "flag", "w_new", "ll1", "lld", "info", "cap", "sig",
+                 "_args", "rc", "ended")
+
+    def __init__(self, eng: Engine, pos, w, sig0, sig1, cap):
+        self.eng = eng
+        self.pos = i32(np.atleast_2d(pos))
+        n, s = self.pos.shape[0], eng.S
+        self.w = f64(w).reshape(n, s, s)
+        self.w_new = np.array(self.w, copy=True)
+        self.w01, self.anc = np.empty((n, s, s)), np.empty((n, s, s))
+        self.flag = np.zeros(n, dtype=np.int32)
+        self.ll1, self.lld = np.empty(n), np.empty(n)
+        self.info = np.empty((n, s, s), dtype=np.int32)
+        self.cap, self.sig = int(cap), (float(sig0), float(sig1))
+        a = _lib.addr
+        self._args = (eng._ctx, n, a(self.pos), a(self.w), float(sig0), float(sig1), int(cap), a(self.w01),
+                      a(self.anc), a(self.w_new), a(self.ll1), a(self.lld), a(self.info), a(self.flag))
+        self.rc, self.ended = None, False
+
+    def run(self):
+        self.rc = _lib.load().nemo_optimal_weights_w(*self._args)
+        self.ended = True
+
+    def begin(self):
+        check(_lib.load().nemo_optimal_weights_w_begin(*self._args))
+
+    def end(self):
+        if not self.ended:
+            self.rc = _lib.load().nemo_optimal_weights_end(self._args[0])
+            self.ended = True
+
+    def recompute(self):
+        """The step again with W~ and ancestor_x made on the host (scipy's
+        expit and inv: chains.inv_stack), synchronously -- no other call may
+        be queued on the engine."""
+        from scipy.special import expit
+
+        from .chains import inv_stack
+        from .nem_order_mcmc import permissible_batch
+        mask = permissible_batch(self.pos, self.cap)
+        sig = self.w.copy()
+        sig[mask] = expit(self.w[mask])
+        eye = np.identity(self.eng.S)
+        self.w01[:] = sig
+        self.anc[:] = np.clip(inv_stack(eye - sig) - eye, 0, 1)
+        self.flag[:] = 0
+        call = _OptimalWeightsCall(self.eng, self.pos, self.w01, self.anc, self.w, *self.sig, self.cap)
+        call.run()
+        self.w_new, self.ll1, self.lld, self.info, self.rc = call.w_new, call.ll1, call.lld, call.info, call.rc
+
+    def result(self, raise_on_fail=True):
+        if self.rc == _lib.NEMO_ERR_LINALG:
+            from scipy.linalg import inv
+            eye = np.identity(self.eng.S)
+            for k in np.nonzero(self.flag)[0]:
+                if self.flag[k] & 3:   # scipy.linalg.inv's own error (LinAlgError / ValueError)
+                    inv(eye - self.w01[k])
+            raise AncestorRecompute(self.rc, _lib.load().nemo_last_error().decode())
+        rc = self.rc
+        if rc == _lib.NEMO_ERR_OPT and not raise_on_fail:
+            return self.w_new, self.ll1, self.lld, self.info
+        if rc == _lib.NEMO_ERR_OPT:
             raise Exception(_lib.load().nemo_last_error().decode())
         check(rc)
         return self.w_new, self.ll1, self.lld, self.info

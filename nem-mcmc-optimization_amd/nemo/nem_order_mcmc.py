@@ -237,16 +237,23 @@ class NEMOrderMCMC:
         while iter_count <= max_iter and ll_diff > abs_diff:
             self.ratio = iter_count / max_iter
             w = self.parent_weights
-            w01 = expit(w)
-            mapped = self.expit_parent_weights(w)
-            self.ancestor_x = np.clip(inv(self.I - mapped) - self.I, 0, 1)
-            self._set_eval1(pos.copy(), w01.copy())
             # init=False re-optimises only the pairs that touch i1 / i2
             # (nem_order_mcmc.py:190-194): the fused call optimises every
             # permissible pair, so a failure raises only on a re-optimised one
-            w_new, ll1, lld, info = self.engine.optimal_weights(
-                pos[None, :], w01[None], self.ancestor_x[None], w[None], SIG0, SIG1, cap=self.cap,
-                raise_on_fail=init)
+            if self.engine.device_ancestor:
+                # W~ = expit on the permissible entries and ancestor_x (:98-103,
+                # :185) made on the device, in scipy's bits
+                w01, anc, w_new, ll1, lld, info = self.engine.optimal_weights_w(
+                    pos[None, :], w[None], SIG0, SIG1, cap=self.cap, raise_on_fail=init)
+                w01, self.ancestor_x = w01[0], anc[0]
+            else:
+                w01 = expit(w)
+                mapped = self.expit_parent_weights(w)
+                self.ancestor_x = np.clip(inv(self.I - mapped) - self.I, 0, 1)
+                w_new, ll1, lld, info = self.engine.optimal_weights(
+                    pos[None, :], w01[None], self.ancestor_x[None], w[None], SIG0, SIG1, cap=self.cap,
+                    raise_on_fail=init)
+            self._set_eval1(pos.copy(), w01.copy())
             w_new = w_new[0]
             if not init:
                 keep = np.zeros_like(self._mask)

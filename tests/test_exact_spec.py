@@ -64,6 +64,33 @@ def test_refmath_host_check_against_the_libraries(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def _scipy_openblas():
+    """(path, architecture) of the OpenBLAS scipy.linalg calls."""
+    import scipy.linalg  # noqa: F401  (loads it)
+    from threadpoolctl import threadpool_info
+    for p in threadpool_info():
+        if p.get("internal_api") == "openblas" and "scipy.libs" in p.get("filepath", ""):
+            return p["filepath"], p.get("architecture")
+    return None, None
+
+
+def test_lapack_inverse_restatement_against_scipys_openblas(tmp_path):
+    """tests/host/lapack_check.c: getrf (n = 1..128) and getri (n <= 64) as
+    csrc/nemo_ancestor.hip restates them, against scipy's own LAPACK calls
+    (scipy_dgetrf_ / scipy_dgetri_, dlopen'ed), to the bit."""
+    gcc = shutil.which("gcc")
+    path, arch = _scipy_openblas()
+    if gcc is None or path is None:
+        pytest.skip("gcc or scipy's OpenBLAS not found")
+    if arch != "SkylakeX":
+        pytest.skip(f"the restatement is of OpenBLAS's SkylakeX kernels (this host: {arch})")
+    exe = str(tmp_path / "lc")
+    subprocess.run([gcc, "-O2", "-ffp-contract=off", os.path.join(HOST, "lapack_check.c"), "-ldl", "-lm",
+                    "-o", exe], check=True)
+    r = subprocess.run([exe, path, "6"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 def test_rcp14_step_function_bucketed_form_is_the_same():
     """svml_log's reduction point r = RNE_1/32(vrcp14pd(m)): the device's
     bucketed lookup (kRcp14Base / kRcp14InBucket) gives the threshold count

@@ -949,19 +949,25 @@ def test_fused_step_graph_replay_equals_direct_launches():
     for a, b, c in zip(g1, g2, d):
         for x, y, z in zip(a, b, c):
             assert np.array_equal(x, z) and np.array_equal(y, z)
-    # an option change between replays takes effect (fp64 eval #2 instead of int8)
-    eng.set_option("graphs", 1)
-    run_all()
-    eng.set_option("fact_kernel", 1)
-    f1 = run_all()
-    eng.set_option("graphs", 0)
-    f0 = run_all()
-    eng.set_option("fact_kernel", 0)
-    for a, c in zip(f1, f0):
-        for x, z in zip(a, c):
-            assert np.array_equal(x, z)
-    assert any(not np.array_equal(a[2], b[2]) for a, b in zip(f0, d))  # ll_dag moved: other kernel
-    eng.set_option("graphs", 1)
+    # an option change between replays takes effect (fp64 eval #2 instead of
+    # int8, on the fast kernels: the exact path takes no fact_kernel)
+    try:
+        eng.set_option("exact", 0)
+        d = run_all()                 # graphs 0, int8
+        eng.set_option("graphs", 1)
+        run_all()
+        eng.set_option("fact_kernel", 1)
+        f1 = run_all()
+        eng.set_option("graphs", 0)
+        f0 = run_all()
+        for a, c in zip(f1, f0):
+            for x, z in zip(a, c):
+                assert np.array_equal(x, z)
+        assert any(not np.array_equal(a[2], b[2]) for a, b in zip(f0, d))  # ll_dag moved: other kernel
+    finally:
+        eng.set_option("fact_kernel", 0)
+        eng.set_option("exact", 1)
+        eng.set_option("graphs", 1)
 
 
 def test_chain_checkpoint_resume_equals_one_run(tmp_path):

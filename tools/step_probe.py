@@ -53,3 +53,5 @@ if os.environ.get("AB_OPT"):
     for v in vals:
         print(f"AB {name}={v} raw ctypes median of rounds {np.median(res[v]):.5f} ms, rounds {np.round(res[v], 5).tolist()}")
     eng.set_option(name, vals[-1])
+# the step from W (W~ and ancestor_x made on the device)
+print("from W (wrapper)", med(lambda: eng.optimal_weights_w(pos, w, SIG0, SIG1, raise_on_fail=False)))
