@@ -164,14 +164,14 @@ def load_record(name, key, build_id):
     if not rec:
         return None
     if rec.get("build_id") == build_id:
-        return rec
+        return dict(rec, matched_by="build_id")
     # a record of another build still holds when the kernel's own translation
     # unit is unchanged (its code id) and the loaded library is the one this
     # tree builds (so that unit's machine code is the one measured)
     from nemo import build as nb
     tu = nb.KERNEL_TU.get(key.split(":")[1])
     if tu and rec.get("code_id") and rec["code_id"] == nb.code_id(tu) and build_id == nb.build_id():
-        return rec
+        return dict(rec, matched_by="code_id")
     return None
 
 
@@ -182,7 +182,7 @@ def stream_roofline(B, bpe, kern_ms, tr):
     the chip's L2 read rate (MI355X_MICROARCH.md: ~34.5 TB/s over the 8
     XCDs).  The 65.5 MB table at C3 stays in the Infinity Cache and the batch
     re-reads each row from the L2, so HBM carries far fewer bytes: those come
-    from the PMC record of this build (FETCH_SIZE x2 + WRITE_SIZE) as a
+    from the PMC record of this kernel's code (FETCH_SIZE x2 + WRITE_SIZE) as a
     fraction of the 8 TB/s HBM peak."""
     ach = B * bpe / (kern_ms / 1e3) / 1e9
     roof = {"bound": "l2", "achieved": ach, "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": ach / L2_PEAK_GBS,
@@ -384,7 +384,7 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
         secondary["hbm"].update({"pmc_bytes_per_launch": traffic["bytes_per_launch"], "pmc_achieved": hbm,
                                  "pmc_frac": hbm / HBM_PEAK_GBS,
                                  "pmc_over_algorithmic": traffic["bytes_per_launch"] / fbytes,
-                                 "pmc_note": "PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, this build) / "
+                                 "pmc_note": "PMC bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, the kernel's code as built here) / "
                                              "this run's launch time"})
     if valu and "SQ_LDS_IDX_ACTIVE" in valu:
         lds = valu["SQ_LDS_IDX_ACTIVE"] / kern_s / 1e12
@@ -394,7 +394,8 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
     roof = {"kernel": KERNEL_NAMES.get(tag, tag), "fact_kernel": fk, "kernel_avg_ms": kern_ms,
             "kernel_avg_ms_launch_events": launch_ev_ms,
             "traffic": traffic["bytes_per_launch"] if traffic else None,
-            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, this build)" if traffic else None,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE of the kernel's code as built "
+                            "here)" if traffic else None,
             "evals_per_launch": B}
     if valu and "SQ_ACTIVE_INST_VALU" in valu:
         busy = 4.0 * valu["SQ_ACTIVE_INST_VALU"]        # SIMD-cycles with a VALU instruction issuing
@@ -405,12 +406,14 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
                      "pmc": {k: valu[k] for k in ("valu_busy", "mfma_busy", "lds_busy", "mfma_coexec_frac",
                                                   "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_MFMA") if k in valu}})
         roof["note"] = ("bound = the SIMD's VALU issue (the exp epilogue: S*E cells per evaluation): achieved = "
-                        "PMC VALU-busy SIMD-cycles per launch of this build (4 x SQ_ACTIVE_INST_VALU) / this run's "
+                        "PMC VALU-busy SIMD-cycles per launch (4 x SQ_ACTIVE_INST_VALU; the record of the kernel's "
+                        f"code as built here, matched by its {valu.get('matched_by', 'build_id')}) / this run's "
                         "HIP-event launch time, against 1024 SIMDs x 2.4 GHz (the max clock, so frac <= the PMC "
                         "valu_busy at the clock the chip held); the other units in secondary")
     elif "int8_mfma" in secondary:
         roof.update({"bound": "mfma", **{k: secondary["int8_mfma"][k] for k in ("achieved", "peak", "unit", "frac")},
-                     "note": "no PMC record of this build (profiles/valu.json): the int8 matrix-core fraction; "
+                     "note": "no PMC record of the kernel's code as built here (profiles/valu.json): the int8 "
+                             "matrix-core fraction; "
                              "the VALU issue binds in every profiled build (DESIGN.md 3.1e)"})
     else:
         roof.update({"bound": "mfma", "achieved": f64eq, "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s",

@@ -161,7 +161,8 @@ int nemo_optimal_weights_end(nemo_ctx* ctx);
  * scipy.linalg.inv's bits (LAPACK getrf + getri of scipy's OpenBLAS 0.3.28,
  * restated in csrc/nemo_ancestor.hip), then runs the step on them.  S <= 64.
  *   w        [nchains][S][S]  the weights W (after the proposal's reset)
- *   w01_out, anc_out [nchains][S][S]  nullable: W~ and ancestor_x
+ *   w01_out, anc_out [nchains][S][S]  nullable: W~ and ancestor_x (both null:
+ *                             neither leaves the device)
  *   anc_flag [nchains]        nullable: 0, or 1 singular / 2 not finite /
  *                             4 non-finite factors (recompute on the host)
  * Returns NEMO_ERR_LINALG when a flag is set (the step's results are then
@@ -294,7 +295,13 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                "exact_lat_waves" (0), the throughput form beyond), 1 latency
  *                (one wave per optimum, two per SIMD), 2 throughput (four per
  *                SIMD), 3 pair (two waves per optimum, the objective's slots
- *                split between them; E > 1024) */
+ *                split between them; E > 1024)
+ *   "anc_overlap" 1 (default): nemo_optimal_weights_w makes ancestor_x on a
+ *                second stream beside eval #1 (same bits); 0 = in line
+ *   "persist_pct" 100 (default): the share (%) of the resident blocks the
+ *                persistent exact local-optimum grid takes -- contexts that
+ *                step side by side (nemo/chains.py's chain groups) split the
+ *                GPU; same bits */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

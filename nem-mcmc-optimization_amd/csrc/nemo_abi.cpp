@@ -165,6 +165,9 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
   for (auto& g : c.step_graph)
     if (g.exec) (void)hipGraphExecDestroy(g.exec);
   (void)hipStreamDestroy(c.stream);
+  if (c.stream2) (void)hipStreamDestroy(c.stream2);
+  if (c.ev_fork) (void)hipEventDestroy(c.ev_fork);
+  if (c.ev_join) (void)hipEventDestroy(c.ev_join);
   delete ctx;
 }
 
@@ -804,7 +807,7 @@ int exact_reserve(Ctx& c, int nchains) {
 int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const double* d_w01,
                             const double* d_anc, double sig0, double sig1, int cap, double* d_w_new,
                             double* d_ll1, double* d_ll_dag, int32_t* d_info, void* stream, double* d_part2,
-                            int* np2) {
+                            int* np2, hipEvent_t anc_ready = nullptr) {
   if (np2) *np2 = 0;
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
@@ -831,6 +834,7 @@ int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, co
     HIPCHK(nemo::launch_step_prep(c, nchains, cap, d_pos, d_w01, d_info, st));
     HIPCHK(nemo::launch_exact_eval(c, nchains, cap, d_pos, d_w01, c.d_ow, cs1, nullptr, true, st,
                                    c.exact_cform == 1 ? c.d_xa : nullptr));
+    if (anc_ready) HIPCHK(hipStreamWaitEvent(st, anc_ready, 0));  // ancestor_x from the second stream
     HIPCHK(nemo::launch_local_opt_exact(c, nchains, nemo::pairs_per_chain(c.S, cap), c.d_pairs, d_w01, d_anc, c.d_ow,
                                         sig0, sig1, d_w_new,
                                         c.d_wdag, d_info, cs1, d_ll1, st));
@@ -855,6 +859,7 @@ int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, co
     HIPCHK(nemo::launch_score(c, nchains, c.d_rows, c.d_sw, c.d_cnt, d_ll1, nullptr, nullptr, c.d_ow, st));
   }
   // every permissible pair's local optimum (nem_order_mcmc.py:186-189)
+  if (anc_ready) HIPCHK(hipStreamWaitEvent(st, anc_ready, 0));
   HIPCHK(nemo::launch_local_opt_pairs(c, nchains, npairs, c.d_pairs, c.d_rows, d_w01, d_anc, c.d_ow,
                                       sig0, sig1, d_w_new, c.d_wdag, d_info, st, fin));
   // eval #2 on the binarised weights (nem_order_mcmc.py:205-207)
@@ -933,7 +938,7 @@ extern "C" {
 // the slot's event; returns without waiting
 static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, const double* w01,
                       const double* anc, const double* w_in, double sig0, double sig1, int cap,
-                      const double* w_new) {
+                      const double* w_new, bool want_prep = false) {
   int rc = check_ctx(ctx, true);
   if (rc) return rc;
   if (nchains < 0) return fail(NEMO_ERR_ARG, "nchains=%d", nchains);
@@ -943,6 +948,11 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   Ctx& c = ctx->c;
   if (from_w && !nemo::ancestor_supported(c))
     return fail(NEMO_ERR_ARG, "S=%d > 64: ancestor_x on the device covers S <= 64 (give W~ and ancestor_x)", c.S);
+  if (from_w && c.anc_overlap && !c.stream2) {  // created before any capture
+    HIPCHK(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
+  }
   if ((rc = check_pos(pos, nchains, c.S))) return rc;
   if ((rc = nemo_reserve(ctx, nchains, nchains))) return rc;
   if (cap >= 0 && step_exact(c, cap) && (rc = exact_reserve(c, nchains))) return rc;
@@ -965,10 +975,25 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   int np2 = 0;
   auto enqueue = [&]() -> int {
     const int32_t* d_pos = (const int32_t*)(ds + L.o_pos);
+    hipEvent_t anc_ready = nullptr;
     if (from_w) {  // [W | pos] in; W~ and ancestor_x made in place
       HIPCHK(hipMemcpyAsync(ds, hs, L.o_w01, hipMemcpyHostToDevice, st));
-      HIPCHK(nemo::launch_ancestor(c, nchains, cap, d_pos, (const double*)ds, (double*)(ds + L.o_w01),
-                                   (double*)(ds + L.o_anc), (int32_t*)(ds + L.o_flag), st));
+      const double* d_w = (const double*)ds;
+      double* d_w01 = (double*)(ds + L.o_w01);
+      double* d_anc = (double*)(ds + L.o_anc);
+      int32_t* d_flag = (int32_t*)(ds + L.o_flag);
+      if (c.anc_overlap) {
+        // W~ on the step's stream for eval #1; ancestor_x on stream2 beside
+        // it, joined before the local optima
+        HIPCHK(nemo::launch_w01(c, nchains, cap, d_pos, d_w, d_w01, st));
+        HIPCHK(hipEventRecord(c.ev_fork, st));
+        HIPCHK(hipStreamWaitEvent(c.stream2, c.ev_fork, 0));
+        HIPCHK(nemo::launch_ancestor(c, nchains, cap, d_pos, d_w, nullptr, d_anc, d_flag, c.stream2));
+        HIPCHK(hipEventRecord(c.ev_join, c.stream2));
+        anc_ready = c.ev_join;
+      } else {
+        HIPCHK(nemo::launch_ancestor(c, nchains, cap, d_pos, d_w, d_w01, d_anc, d_flag, st));
+      }
     } else {  // info: preset by the prep
       HIPCHK(hipMemcpyAsync(ds + L.o_pos, hs + L.o_pos, L.o_wn - L.o_pos, hipMemcpyHostToDevice, st));
     }
@@ -976,9 +1001,10 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
                                     (const double*)(ds + L.o_anc), sig0, sig1, cap, (double*)(ds + L.o_wn),
                                     (double*)(ds + L.o_ll1), (double*)(ds + L.o_lld), (int32_t*)(ds + L.o_inf), st,
                                     c.step_host_sum && L.o_part < L.total ? (double*)(ds + L.o_part) : nullptr,
-                                    &np2);
+                                    &np2, anc_ready);
     if (r) return r;  // np2 <= step_npart: checked by launch_score_factored before it launched
-    const size_t o_out = from_w ? L.o_w01 : L.o_wn;
+    // W~ and ancestor_x go back only when the caller asked for them
+    const size_t o_out = from_w && want_prep ? L.o_w01 : L.o_wn;
     HIPCHK(hipMemcpyAsync(hs + o_out, ds + o_out, L.total - o_out, hipMemcpyDeviceToHost, st));
     return NEMO_OK;
   };
@@ -987,7 +1013,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if (c.graphs && !c.timing) {
     for (auto& g : c.step_graph)
       if (g.exec && g.epoch == c.graph_epoch && g.nchains == nchains && g.cap == cap && g.slot == slot &&
-          g.sig0 == sig0 && g.sig1 == sig1 && g.from_w == from_w)
+          g.sig0 == sig0 && g.sig1 == sig1 && g.from_w == from_w && g.want_prep == want_prep)
         sg = &g;
     if (!sg) {  // capture once
       Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
@@ -1018,6 +1044,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
           g.sig0 = sig0;
           g.sig1 = sig1;
           g.from_w = from_w;
+          g.want_prep = want_prep;
           g.epoch = c.graph_epoch;
           g.np2 = np2;
           sg = &g;
@@ -1111,7 +1138,7 @@ int nemo_optimal_weights_w(nemo_ctx* ctx, int nchains, const int32_t* pos, const
                            double sig1, int cap, double* w01_out, double* anc_out, double* w_new, double* ll1,
                            double* ll_dag, int32_t* info, int32_t* anc_flag) {
   if (!ll1 || !ll_dag || !w) return fail(NEMO_ERR_ARG, "null host pointer");
-  int rc = step_start(ctx, 0, nchains, pos, nullptr, nullptr, w, sig0, sig1, cap, w_new);
+  int rc = step_start(ctx, 0, nchains, pos, nullptr, nullptr, w, sig0, sig1, cap, w_new, w01_out || anc_out);
   if (rc) return rc;
   return step_finish(ctx, 0, nchains, w_new, ll1, ll_dag, info, true, w01_out, anc_out, anc_flag);
 }
@@ -1159,7 +1186,7 @@ static int steps_submit(nemo_ctx* ctx, std::unique_ptr<StepJob> j) {
           [ctx, next_slot](StepJob& j) {  // start: true = in flight
             j.slot = *next_slot;
             j.rc = step_start(ctx, j.slot, j.nchains, j.pos, j.w01, j.anc, j.w_in, j.sig0, j.sig1, j.cap,
-                              j.w_new);
+                              j.w_new, j.w01_out || j.anc_out);
             if (j.rc) {
               j.err = g_err;
               (void)hipStreamSynchronize(ctx->c.stream);  // nothing of it left running in its slot
@@ -1396,6 +1423,15 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.exact_sched = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "anc_overlap") == 0) {
+    ctx->c.anc_overlap = value ? 1 : 0;
+    return NEMO_OK;
+  }
+  if (strcmp(name, "persist_pct") == 0) {
+    if (value < 1 || value > 100) return fail(NEMO_ERR_ARG, "persist_pct %d outside [1, 100]", value);
+    ctx->c.exact_persist_pct = value;
+    return NEMO_OK;
+  }
   if (strcmp(name, "exact_persist") == 0) {
     ctx->c.exact_persist = value ? 1 : 0;
     return NEMO_OK;
@@ -1477,6 +1513,8 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact_trace") == 0) *value = c.exact_trace;
   else if (strcmp(name, "exact_persist") == 0) *value = c.exact_persist;
   else if (strcmp(name, "exact_sched") == 0) *value = c.exact_sched;
+  else if (strcmp(name, "anc_overlap") == 0) *value = c.anc_overlap;
+  else if (strcmp(name, "persist_pct") == 0) *value = c.exact_persist_pct;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;

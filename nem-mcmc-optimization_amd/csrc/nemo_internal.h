@@ -28,6 +28,14 @@ struct Ctx {
   int device = 0;
   int S = 0, E = 0, dtype = 0;     // dtype: 0 f64, 1 f32
   hipStream_t stream = nullptr;
+  // nemo_optimal_weights_w: ancestor_x on stream2 beside eval #1 (option
+  // "anc_overlap"), forked and joined through these events
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int anc_overlap = 1;
+  // option "persist_pct": the persistent local-optimum grid takes this share
+  // of the resident blocks (engines that step side by side split the GPU)
+  int exact_persist_pct = 100;
   bool staged = false;
   int xcd_remap = 1;               // option "xcd_remap": XCD-aware block order
   double table_absmax = 0.0;       // max |T| over off-diagonal rows
@@ -199,6 +207,7 @@ struct Ctx {
     int np2 = 0;                   // eval #2's partials per chain left for the host (0: ll_dag on device)
     double sig0 = 0.0, sig1 = 0.0;
     bool from_w = false;           // nemo_optimal_weights_w: ancestor_x made on the device
+    bool want_prep = false;        // ... and W~ / ancestor_x copied back
     uint64_t epoch = 0;
     hipGraphExec_t exec = nullptr;
   };
@@ -528,5 +537,9 @@ int resolve_fact_kernel(const Ctx& c, int cap, bool ll_only, double* bound);
 bool ancestor_supported(const Ctx& c);
 hipError_t launch_ancestor(Ctx& c, int nchains, int cap, const int32_t* d_pos, const double* d_w, double* d_w01,
                            double* d_anc, int32_t* d_flag, hipStream_t st);
+// W~ alone (d_w01), for a step whose ancestor_x runs on a second stream
+// (launch_ancestor with d_w01 null)
+hipError_t launch_w01(Ctx& c, int nchains, int cap, const int32_t* d_pos, const double* d_w, double* d_w01,
+                      hipStream_t st);
 
 }  // namespace nemo

@@ -139,11 +139,11 @@ def _device_step(engine: Engine, prep, cap, raise_on_fail):
 
 
 def _finish(chains, engine: Engine, prep, res, use_nem, cap):
-    pos, _w, w01, _anc = prep
+    pos, _w, w01, _anc = prep   # w01 None: made from W when the chain's order weights are read
     w_new, ll1, lld, _ = res
     out = np.empty(len(chains))
     for k, c in enumerate(chains):
-        c._set_eval1(pos[k], w01[k])
+        c._set_eval1(pos[k], None if w01 is None else w01[k], _w[k])
         c.parent_weights = w_new[k]   # a fresh array per call: the views are private
         c.ll = float(ll1[k])
         if use_nem:
@@ -176,7 +176,10 @@ def _w_call_end(chains, call, raise_on_fail, drain=None):
         res = call.result(raise_on_fail)
     for k, c in enumerate(chains):
         c.ll = 0.0
-        c.ancestor_x = call.anc[k]
+        if call.anc is not None:
+            c.ancestor_x = call.anc[k]
+        else:   # made on the host, same bits, if ever read
+            c._set_ancestor_src(call.pos[k], call.w[k])
     return (call.pos, call.w, call.w01, call.anc), res
 
 
@@ -190,7 +193,7 @@ def optimal_weights_batch(chains, engine: Engine, use_nem=False, cap=0, raise_on
     if _device_ancestor(engine, pool):
         pos = np.stack([c._pos for c in chains]).astype(np.int32)
         w = np.stack([c.parent_weights for c in chains])
-        call = engine.bind_optimal_weights_w(pos, w, SIG0, SIG1, cap=cap)
+        call = engine.bind_optimal_weights_w(pos, w, SIG0, SIG1, cap=cap, want_prep=False)
         call.run()
         prep, res = _w_call_end(chains, call, raise_on_fail)
         return _finish(chains, engine, prep, res, use_nem, cap)
@@ -289,7 +292,11 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     # next order: with raise_on_fail the exception leaves the chains' states
     # (orders, weights, RNG streams) unspecified -- only the results of runs
     # that complete are defined to equal a sequential batched run.
-    n_groups = 1 if (use_nem or n < 2) else (groups or (3 if n >= 6 else 2))
+    dev = _device_ancestor(engine, pool)
+    # device ancestor_x: two groups, each on its own engine context (a clone:
+    # own buffers and stream), so one group's step runs on the GPU beside the
+    # other's while the host works; host ancestor_x: groups on one context
+    n_groups = 1 if (use_nem or n < 2) else (groups or (2 if dev else 3 if n >= 6 else 2))
     n_groups = max(1, min(n_groups, n))
     bounds = [n * g // n_groups for g in range(n_groups + 1)]
     glist = [list(range(bounds[g], bounds[g + 1])) for g in range(n_groups)]
@@ -303,7 +310,10 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         pending = deque()
         wst = [None] * n_groups     # each group's weights stack (its last step's w_new)
         early = n_groups >= 3       # finish the oldest group before queuing the next
-        dev = _device_ancestor(engine, pool)
+        engs = engine.group_engines(n_groups) if dev else [engine] * n_groups
+        if dev:   # the groups' local-optimum grids split the GPU
+            for e in engs:
+                e.set_option("persist_pct", max(1, 100 // n_groups))
 
         def drain():
             for p in pending:
@@ -329,8 +339,8 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                         while early and len(pending) > n_groups - 2:
                             collect()
                         prep = None
-                        call = engine.bind_optimal_weights_w(stacks[0].astype(np.int32), stacks[1], SIG0, SIG1,
-                                                             cap=cap)
+                        call = engs[g].bind_optimal_weights_w(stacks[0].astype(np.int32), stacks[1], SIG0, SIG1,
+                                                              cap=cap, want_prep=False)
                     else:
                         part = _prepare_start(cs, pool, stacks)
                         while early and len(pending) > n_groups - 2:
@@ -347,6 +357,9 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         finally:
             for p in pending:   # an exception left queued steps: wait for them
                 p[3].end()
+            if dev:
+                for e in engs:
+                    e.set_option("persist_pct", 100)
     for k, c in enumerate(chains):
         q = st[k]
         c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]

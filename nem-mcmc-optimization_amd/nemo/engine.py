@@ -43,6 +43,7 @@ class Engine:
             raise ValueError(f"U must be ({S + 1}, {E}), got {U.shape}")
         self._create(S, E, device, dtype)
         check(_lib.load().nemo_stage_tables(self._ctx, ptr(U), ptr(T)))
+        self._stage = ("tables", U, T)
 
     def _create(self, S, E, device, dtype):
         lib = _lib.load()
@@ -67,7 +68,45 @@ class Engine:
         self._create(d8.shape[0], d8.shape[1], device, dtype)
         check(_lib.load().nemo_stage_knockdown(self._ctx, d8.ctypes.data_as(_lib._u8p),
                                                float(A), float(B)))
+        self._stage = ("knockdown", d8, float(A), float(B))
         return self
+
+    # options a clone carries over (the settable ones of include/nemo.h)
+    _CLONED_OPTIONS = ("xcd_remap", "score_path", "fact_kernel", "i8o_nodiag", "graphs", "step_host_sum",
+                       "local_split", "exact", "exact_dev", "exact_form", "exact_pair_waves", "exact_lat_waves",
+                       "exact_cform", "exact_xcd", "exact_persist", "exact_sched", "anc_overlap", "persist_pct")
+
+    def clone(self) -> "Engine":
+        """Another context on the same device with the same staged model and
+        options: its own buffers, stream and step thread, so two clones' steps
+        run side by side on the GPU (nemo/chains.py's chain groups)."""
+        kind, *args = self._stage
+        if kind == "knockdown":
+            e = Engine.from_knockdown(*args, device=self.device, dtype=self.dtype)
+        else:
+            e = Engine(*args, device=self.device, dtype=self.dtype)
+        self._copy_options_to(e)
+        return e
+
+    def _copy_options_to(self, e: "Engine"):
+        for name in self._CLONED_OPTIONS:
+            try:
+                v = self.get_option(name)
+                if e.get_option(name) != v:
+                    e.set_option(name, v)
+            except _lib.NemoError:
+                pass
+        e.set_option_f64("err_budget", self.get_option_f64("err_budget"))
+
+    def group_engines(self, n: int):
+        """This engine and n - 1 clones of it (made once, kept; their options
+        brought to this engine's on every call)."""
+        clones = self.__dict__.setdefault("_clones", [])
+        while len(clones) < n - 1:
+            clones.append(self.clone())
+        for e in clones[:n - 1]:
+            self._copy_options_to(e)
+        return [self] + clones[:n - 1]
 
     # -- cached engines per model -----------------------------------------
     @classmethod
@@ -194,10 +233,11 @@ class Engine:
             res = call.result(raise_on_fail)
         return (call.w01, call.anc) + res
 
-    def bind_optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0):
+    def bind_optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0, want_prep=True):
         """``optimal_weights_w`` in parts, as ``bind_optimal_weights``; the
-        call's ``w01`` / ``anc`` hold W~ and ancestor_x once it has ended."""
-        return _OptimalWeightsWCall(self, pos, w, sig0, sig1, cap)
+        call's ``w01`` / ``anc`` hold W~ and ancestor_x once it has ended
+        (``want_prep=False``: None, neither leaves the device)."""
+        return _OptimalWeightsWCall(self, pos, w, sig0, sig1, cap, want_prep)
 
     # -- fixed-order optimizers (methods.py) --------------------------------
     def _sweep(self, fn, pos, w, *extra, raise_on_fail=True):
@@ -392,20 +432,21 @@ class _OptimalWeightsWCall:
     __slots__ = ("eng", "pos", "w", "w01", "anc", "flag", "w_new", "ll1", "lld", "info", "cap", "sig",
                  "_args", "rc", "ended")
 
-    def __init__(self, eng: Engine, pos, w, sig0, sig1, cap):
+    def __init__(self, eng: Engine, pos, w, sig0, sig1, cap, want_prep=True):
         self.eng = eng
         self.pos = i32(np.atleast_2d(pos))
         n, s = self.pos.shape[0], eng.S
         self.w = f64(w).reshape(n, s, s)
         self.w_new = np.array(self.w, copy=True)
-        self.w01, self.anc = np.empty((n, s, s)), np.empty((n, s, s))
+        self.w01, self.anc = (np.empty((n, s, s)), np.empty((n, s, s))) if want_prep else (None, None)
         self.flag = np.zeros(n, dtype=np.int32)
         self.ll1, self.lld = np.empty(n), np.empty(n)
         self.info = np.empty((n, s, s), dtype=np.int32)
         self.cap, self.sig = int(cap), (float(sig0), float(sig1))
         a = _lib.addr
-        self._args = (eng._ctx, n, a(self.pos), a(self.w), float(sig0), float(sig1), int(cap), a(self.w01),
-                      a(self.anc), a(self.w_new), a(self.ll1), a(self.lld), a(self.info), a(self.flag))
+        self._args = (eng._ctx, n, a(self.pos), a(self.w), float(sig0), float(sig1), int(cap),
+                      None if self.w01 is None else a(self.w01), None if self.anc is None else a(self.anc),
+                      a(self.w_new), a(self.ll1), a(self.lld), a(self.info), a(self.flag))
         self.rc, self.ended = None, False
 
     def run(self):
@@ -424,28 +465,34 @@ class _OptimalWeightsWCall:
         """The step again with W~ and ancestor_x made on the host (scipy's
         expit and inv: chains.inv_stack), synchronously -- no other call may
         be queued on the engine."""
-        from scipy.special import expit
-
         from .chains import inv_stack
-        from .nem_order_mcmc import permissible_batch
-        mask = permissible_batch(self.pos, self.cap)
-        sig = self.w.copy()
-        sig[mask] = expit(self.w[mask])
+        sig = self.host_w01()
         eye = np.identity(self.eng.S)
-        self.w01[:] = sig
-        self.anc[:] = np.clip(inv_stack(eye - sig) - eye, 0, 1)
+        self.w01 = sig
+        self.anc = np.clip(inv_stack(eye - sig) - eye, 0, 1)
         self.flag[:] = 0
         call = _OptimalWeightsCall(self.eng, self.pos, self.w01, self.anc, self.w, *self.sig, self.cap)
         call.run()
         self.w_new, self.ll1, self.lld, self.info, self.rc = call.w_new, call.ll1, call.lld, call.info, call.rc
 
+    def host_w01(self):
+        """W~ as the host makes it (scipy's expit on the permissible entries)."""
+        from scipy.special import expit
+
+        from .nem_order_mcmc import permissible_batch
+        mask = permissible_batch(self.pos, self.cap)
+        sig = self.w.copy()
+        sig[mask] = expit(self.w[mask])
+        return sig
+
     def result(self, raise_on_fail=True):
         if self.rc == _lib.NEMO_ERR_LINALG:
             from scipy.linalg import inv
             eye = np.identity(self.eng.S)
+            w01 = self.w01 if self.w01 is not None else self.host_w01()
             for k in np.nonzero(self.flag)[0]:
                 if self.flag[k] & 3:   # scipy.linalg.inv's own error (LinAlgError / ValueError)
-                    inv(eye - self.w01[k])
+                    inv(eye - w01[k])
             raise AncestorRecompute(self.rc, _lib.load().nemo_last_error().decode())
         rc = self.rc
         if rc == _lib.NEMO_ERR_OPT and not raise_on_fail:

@@ -116,7 +116,9 @@ class NEMOrderMCMC:
         self.cell_ratios = self.compute_cell_ratios(self.parent_weights, self.score_tables)
         self.perm_order = perm_order
         self.I = np.identity(self.num_s)
-        self._eval1 = None      # (pos, expit(W)) of the last eval #1
+        self._eval1 = None      # (pos, W~ or None, W) of the last eval #1
+        self._anc = None        # ancestor_x (or where to make it: _anc_src)
+        self._anc_src = None
         self._ow = None         # its order weights, computed on first access
 
     # -- A3 / A7: parent sets and the reset quirks ---------------------------
@@ -289,9 +291,33 @@ class NEMOrderMCMC:
             dag_ll = float(self.engine.score(pos[None, :], w01d[None], cap=self.cap)[0])
         return dag_ll
 
-    def _set_eval1(self, pos, w01):
-        self._eval1 = (pos, w01)
+    def _set_eval1(self, pos, w01, w=None):
+        """The last eval #1's (pos, W~); W~ None: made from W when needed
+        (expit of W -- the score reads the permissible entries only)."""
+        self._eval1 = (pos, w01, w)
         self._ow = None
+
+    @property
+    def ancestor_x(self):
+        """clip(inv(I - W~) - I, 0, 1) of the last step (nem_order_mcmc.py:185).
+        A chain batch whose device made it leaves where it came from: the
+        host makes the same bits (scipy's expit and inv) on first access."""
+        if self._anc is None and self._anc_src is not None:
+            pos, w = self._anc_src
+            mask = self._permissible(pos)
+            sig = np.array(w, dtype=np.float64, copy=True)
+            sig[mask] = expit(sig[mask])
+            self._anc = np.clip(inv(self.I - sig) - self.I, 0, 1)
+            self._anc_src = None
+        return self._anc
+
+    @ancestor_x.setter
+    def ancestor_x(self, value):
+        self._anc = value
+        self._anc_src = None
+
+    def _set_ancestor_src(self, pos, w):
+        self._anc, self._anc_src = None, (pos, w)
 
     @property
     def order_weights(self):
@@ -303,7 +329,9 @@ class NEMOrderMCMC:
             if self._eval1 is None:
                 raise AttributeError("'NEMOrderMCMC' object has no attribute 'order_weights' "
                                      "(set by get_optimal_weights)")
-            pos, w01 = self._eval1
+            pos, w01, w = self._eval1
+            if w01 is None:
+                w01 = expit(np.asarray(w, dtype=np.float64))
             self._ow = self.engine.score(pos[None, :], w01[None], cap=self.cap, want_ow=True)["ow"][0]
         return self._ow
 

@@ -103,12 +103,15 @@ def test_ancestor_flags_and_scipys_errors():
     eng.close()
 
 
-@pytest.mark.parametrize("cap", [0, 3])
-def test_step_from_w_equals_step_from_host_ancestor(cap):
+@pytest.mark.parametrize("cap,overlap", [(0, 1), (3, 1), (0, 0)])
+def test_step_from_w_equals_step_from_host_ancestor(cap, overlap):
     """nemo_optimal_weights_w (W in) against nemo_optimal_weights with the
-    host's W~ / ancestor_x: every output to the bit, direct and queued."""
+    host's W~ / ancestor_x: every output to the bit, direct and queued, with
+    ancestor_x beside eval #1 on a second stream (option anc_overlap 1, the
+    default) or in line."""
     m = generator.config_nem("C3")
     eng = Engine.for_nem(m)
+    eng.set_option("anc_overlap", overlap)
     rng = np.random.default_rng(21 + cap)
     n = 16
     pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)

@@ -832,7 +832,7 @@ def test_order_weights_per_sampler_on_shared_engine():
     # method() on a shared engine leaves a usable order_weights
     random.seed(5)
     a.method(n_iterations=3, gamma=0.05, verbose=False)
-    pos, w01 = a._eval1
+    pos, w01, _ = a._eval1
     ref = no.calculate_ll(no.cell_ratios(m.U, t, no.parents_of(np.argsort(pos)), w01))[0]
     assert np.max(np.abs(a.order_weights - ref)) <= 1e-11
 

@@ -1,5 +1,5 @@
 import sys, time, os
-sys.path.insert(0, "nem-mcmc-optimization_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "nem-mcmc-optimization_amd"))
 import numpy as np, torch, ctypes as C
 from scipy.special import expit
 from nemo import generator, _lib
