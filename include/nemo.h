@@ -297,11 +297,7 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                SIMD), 3 pair (two waves per optimum, the objective's slots
  *                split between them; E > 1024)
  *   "anc_overlap" 1 (default): nemo_optimal_weights_w makes ancestor_x on a
- *                second stream beside eval #1 (same bits); 0 = in line
- *   "persist_pct" 100 (default): the share (%) of the resident blocks the
- *                persistent exact local-optimum grid takes -- contexts that
- *                step side by side (nemo/chains.py's chain groups) split the
- *                GPU; same bits */
+ *                second stream beside eval #1 (same bits); 0 = in line */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);
 int nemo_get_option(nemo_ctx* ctx, const char* name, int* value);
 

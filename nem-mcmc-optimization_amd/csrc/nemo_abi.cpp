@@ -1427,11 +1427,6 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.anc_overlap = value ? 1 : 0;
     return NEMO_OK;
   }
-  if (strcmp(name, "persist_pct") == 0) {
-    if (value < 1 || value > 100) return fail(NEMO_ERR_ARG, "persist_pct %d outside [1, 100]", value);
-    ctx->c.exact_persist_pct = value;
-    return NEMO_OK;
-  }
   if (strcmp(name, "exact_persist") == 0) {
     ctx->c.exact_persist = value ? 1 : 0;
     return NEMO_OK;
@@ -1514,7 +1509,6 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact_persist") == 0) *value = c.exact_persist;
   else if (strcmp(name, "exact_sched") == 0) *value = c.exact_sched;
   else if (strcmp(name, "anc_overlap") == 0) *value = c.anc_overlap;
-  else if (strcmp(name, "persist_pct") == 0) *value = c.exact_persist_pct;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;
   else if (strcmp(name, "exact_pair_waves") == 0) *value = c.exact_pair_waves;
   else if (strcmp(name, "exact_ok") == 0) *value = nemo::exact_supported(c) ? 1 : 0;

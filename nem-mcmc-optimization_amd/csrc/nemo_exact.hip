@@ -1123,7 +1123,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
       case 8: res = lo_resident_ns<8>(form, rc); break;
       default: return hipErrorInvalidValue;
     }
-    lo_blocks = std::min(lo_blocks, std::max(res * c.exact_persist_pct / 100, 1));
+    lo_blocks = std::min(lo_blocks, std::max(res, 1));
     const hipError_t me = hipMemsetAsync(c.d_xqueue, 0, sizeof(int), st);
     if (me != hipSuccess) return me;
   }

@@ -33,9 +33,6 @@ struct Ctx {
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int anc_overlap = 1;
-  // option "persist_pct": the persistent local-optimum grid takes this share
-  // of the resident blocks (engines that step side by side split the GPU)
-  int exact_persist_pct = 100;
   bool staged = false;
   int xcd_remap = 1;               // option "xcd_remap": XCD-aware block order
   double table_absmax = 0.0;       // max |T| over off-diagonal rows

@@ -293,10 +293,12 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     # (orders, weights, RNG streams) unspecified -- only the results of runs
     # that complete are defined to equal a sequential batched run.
     dev = _device_ancestor(engine, pool)
-    # device ancestor_x: two groups, each on its own engine context (a clone:
-    # own buffers and stream), so one group's step runs on the GPU beside the
-    # other's while the host works; host ancestor_x: groups on one context
-    n_groups = 1 if (use_nem or n < 2) else (groups or (2 if dev else 3 if n >= 6 else 2))
+    # device ancestor_x: one group by default -- a group's step carries the
+    # inversion's fixed latency, so splitting the chains costs more device time
+    # than the host work it hides (2.38 ms per 16-chain step in one
+    # group, 2.94 in two, 3.42 in three); host ancestor_x: groups hide the
+    # pool's inversions
+    n_groups = 1 if (use_nem or n < 2) else (groups or (1 if dev else 3 if n >= 6 else 2))
     n_groups = max(1, min(n_groups, n))
     bounds = [n * g // n_groups for g in range(n_groups + 1)]
     glist = [list(range(bounds[g], bounds[g + 1])) for g in range(n_groups)]
@@ -310,10 +312,6 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         pending = deque()
         wst = [None] * n_groups     # each group's weights stack (its last step's w_new)
         early = n_groups >= 3       # finish the oldest group before queuing the next
-        engs = engine.group_engines(n_groups) if dev else [engine] * n_groups
-        if dev:   # the groups' local-optimum grids split the GPU
-            for e in engs:
-                e.set_option("persist_pct", max(1, 100 // n_groups))
 
         def drain():
             for p in pending:
@@ -339,8 +337,8 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
                         while early and len(pending) > n_groups - 2:
                             collect()
                         prep = None
-                        call = engs[g].bind_optimal_weights_w(stacks[0].astype(np.int32), stacks[1], SIG0, SIG1,
-                                                              cap=cap, want_prep=False)
+                        call = engine.bind_optimal_weights_w(stacks[0].astype(np.int32), stacks[1], SIG0, SIG1,
+                                                             cap=cap, want_prep=False)
                     else:
                         part = _prepare_start(cs, pool, stacks)
                         while early and len(pending) > n_groups - 2:
@@ -357,9 +355,7 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
         finally:
             for p in pending:   # an exception left queued steps: wait for them
                 p[3].end()
-            if dev:
-                for e in engs:
-                    e.set_option("persist_pct", 100)
+
     for k, c in enumerate(chains):
         q = st[k]
         c.best_score, c.best_dag, c.best_order = q["best"], q["best_dag"], q["best_order"]

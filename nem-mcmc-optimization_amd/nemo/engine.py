@@ -43,7 +43,6 @@ class Engine:
             raise ValueError(f"U must be ({S + 1}, {E}), got {U.shape}")
         self._create(S, E, device, dtype)
         check(_lib.load().nemo_stage_tables(self._ctx, ptr(U), ptr(T)))
-        self._stage = ("tables", U, T)
 
     def _create(self, S, E, device, dtype):
         lib = _lib.load()
@@ -68,45 +67,7 @@ class Engine:
         self._create(d8.shape[0], d8.shape[1], device, dtype)
         check(_lib.load().nemo_stage_knockdown(self._ctx, d8.ctypes.data_as(_lib._u8p),
                                                float(A), float(B)))
-        self._stage = ("knockdown", d8, float(A), float(B))
         return self
-
-    # options a clone carries over (the settable ones of include/nemo.h)
-    _CLONED_OPTIONS = ("xcd_remap", "score_path", "fact_kernel", "i8o_nodiag", "graphs", "step_host_sum",
-                       "local_split", "exact", "exact_dev", "exact_form", "exact_pair_waves", "exact_lat_waves",
-                       "exact_cform", "exact_xcd", "exact_persist", "exact_sched", "anc_overlap", "persist_pct")
-
-    def clone(self) -> "Engine":
-        """Another context on the same device with the same staged model and
-        options: its own buffers, stream and step thread, so two clones' steps
-        run side by side on the GPU (nemo/chains.py's chain groups)."""
-        kind, *args = self._stage
-        if kind == "knockdown":
-            e = Engine.from_knockdown(*args, device=self.device, dtype=self.dtype)
-        else:
-            e = Engine(*args, device=self.device, dtype=self.dtype)
-        self._copy_options_to(e)
-        return e
-
-    def _copy_options_to(self, e: "Engine"):
-        for name in self._CLONED_OPTIONS:
-            try:
-                v = self.get_option(name)
-                if e.get_option(name) != v:
-                    e.set_option(name, v)
-            except _lib.NemoError:
-                pass
-        e.set_option_f64("err_budget", self.get_option_f64("err_budget"))
-
-    def group_engines(self, n: int):
-        """This engine and n - 1 clones of it (made once, kept; their options
-        brought to this engine's on every call)."""
-        clones = self.__dict__.setdefault("_clones", [])
-        while len(clones) < n - 1:
-            clones.append(self.clone())
-        for e in clones[:n - 1]:
-            self._copy_options_to(e)
-        return [self] + clones[:n - 1]
 
     # -- cached engines per model -----------------------------------------
     @classmethod

@@ -33,7 +33,7 @@ def main():
             eng.optimal_weights_w(pos, w, SIG0, SIG1, raise_on_fail=False)
             ts.append(time.perf_counter() - t0)
         print(f"anc_overlap {ov}: fused step from W {1e3 * np.median(ts):.3f} ms", flush=True)
-        for g in (1, 2, 3, 4):
+        for g in (1, 2, 3):
             ChainBatch(m, [order] * n, seeds=seeds, engine=eng, on_fail="continue", groups=g).run(2)
             walls = []
             for _ in range(3):
