@@ -405,6 +405,15 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
                      "frac": a / peak, "valu_busy_cycles_per_launch": busy,
                      "pmc": {k: valu[k] for k in ("valu_busy", "mfma_busy", "lds_busy", "mfma_coexec_frac",
                                                   "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_MFMA") if k in valu}})
+        if tag == "i8l":
+            # the formulation's own work: the epilogue's 11 VALU per cell, S x E
+            # cells per evaluation, one wave instruction per 64 cells at 4 SIMD-cycles each, priced
+            # at the same max-clock issue rate; the rest of the 16.6 per 64 cells is 3.1i's table
+            alg = 4.0 * 11.0 * S * E / 64.0 * B
+            roof["algorithmic_frac"] = alg / kern_s / (N_SIMD * CLOCK_MAX_GHZ * 1e9)
+            roof["algorithmic_valu_per_64_cells"] = 11.0
+            if "SQ_INSTS_VALU" in valu:
+                roof["valu_per_64_cells"] = valu["SQ_INSTS_VALU"] / (B * S * E / 64.0)
         roof["note"] = ("bound = the SIMD's VALU issue (the exp epilogue: S*E cells per evaluation): achieved = "
                         "PMC VALU-busy SIMD-cycles per launch (4 x SQ_ACTIVE_INST_VALU; the record of the kernel's "
                         f"code as built here, matched by its {valu.get('matched_by', 'build_id')}) / this run's "

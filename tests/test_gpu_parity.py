@@ -747,6 +747,7 @@ def test_integration_stub_binds_the_library(net2):
     want = ref.get_optimal_weights(init=True)
     got = scorer.optimal_weights(smp)
     assert got == want and np.array_equal(smp.parent_weights, ref.parent_weights)  # same kernels, same bits
+    assert np.array_equal(smp.ancestor_x, ref.ancestor_x)
     _ow, ll = scorer.order_score(smp)
     assert abs(ll - float(ref.engine.score(ref._pos[None], expit(ref.parent_weights)[None])[0])) <= 1e-9
 

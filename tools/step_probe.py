@@ -6,7 +6,7 @@ from nemo import generator, _lib
 from nemo.engine import Engine
 from nemo.nem_order_mcmc import SIG0, SIG1
 m = generator.config_nem("C3"); eng = Engine.for_nem(m)
-for opt in ("graphs", "local_split", "exact", "exact_cform", "exact_xcd", "exact_form"):
+for opt in ("graphs", "local_split", "exact", "exact_cform", "exact_xcd", "exact_form", "anc_overlap"):
     if opt.upper() in os.environ:
         eng.set_option(opt, int(os.environ[opt.upper()]))
 S = 64; n = int(sys.argv[1]) if len(sys.argv) > 1 else 16
