@@ -645,8 +645,9 @@ def main():
                 if given_anc:
                     eng.optimal_weights(pos_h[:nc], expit(w_h[:nc]), anc[:nc], w_h[:nc], SIG0, SIG1, cap=cap,
                                         raise_on_fail=False)
-                else:
-                    eng.optimal_weights_w(pos_h[:nc], w_h[:nc], SIG0, SIG1, cap=cap, raise_on_fail=False)
+                else:   # as the chain batch calls it: W~ / ancestor_x stay on the device
+                    eng.optimal_weights_w(pos_h[:nc], w_h[:nc], SIG0, SIG1, cap=cap, raise_on_fail=False,
+                                          want_prep=False)
             call()
             ts = []
             for _ in range(reps):
@@ -693,7 +694,7 @@ def main():
         ts1 = []
         for _ in range(20):
             t0 = time.perf_counter()
-            eng.optimal_weights_w(pos_h[:1], w_h[:1], SIG0, SIG1, cap=cap, raise_on_fail=False)
+            eng.optimal_weights_w(pos_h[:1], w_h[:1], SIG0, SIG1, cap=cap, raise_on_fail=False)   # as the sampler
             ts1.append(time.perf_counter() - t0)
         extras["single_chain"] = {
             "score_call_us": 1e6 * float(np.median(lat)), "evals_per_s_sequential": 1.0 / float(np.median(lat)),

@@ -181,11 +181,12 @@ class Engine:
         ancestor_x made on the device in scipy's bits (S <= 64)."""
         return self.S <= 64
 
-    def optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0, raise_on_fail=True):
+    def optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0, raise_on_fail=True, want_prep=True):
         """``optimal_weights`` from the weights themselves: the device makes
         W~ and ancestor_x (nem_order_mcmc.py:98-103, :185) as scipy does.
-        Returns (w01, anc, w_new, ll1, ll_dag, info)."""
-        call = self.bind_optimal_weights_w(pos, w, sig0, sig1, cap=cap)
+        Returns (w01, anc, w_new, ll1, ll_dag, info); w01 / anc None with
+        ``want_prep=False`` (they stay on the device)."""
+        call = self.bind_optimal_weights_w(pos, w, sig0, sig1, cap=cap, want_prep=want_prep)
         call.run()
         try:
             res = call.result(raise_on_fail)
