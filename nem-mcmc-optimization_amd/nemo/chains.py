@@ -293,12 +293,13 @@ def run_methods(chains, gammas, n_iterations, engine: Engine, swap_prob=0.95, us
     # (orders, weights, RNG streams) unspecified -- only the results of runs
     # that complete are defined to equal a sequential batched run.
     dev = _device_ancestor(engine, pool)
-    # device ancestor_x: one group by default -- a group's step carries the
-    # inversion's fixed latency, so splitting the chains costs more device time
-    # than the host work it hides (2.38 ms per 16-chain step in one
-    # group, 2.94 in two, 3.42 in three); host ancestor_x: groups hide the
-    # pool's inversions
-    n_groups = 1 if (use_nem or n < 2) else (groups or (1 if dev else 3 if n >= 6 else 2))
+    # device ancestor_x: one group up to 32 chains -- a group's step carries the
+    # inversion's fixed latency, so splitting few chains costs more device time
+    # than the host work it hides (16 chains: 2.38 ms per step in one group,
+    # 2.94 in two; 32: 4.33 / 4.44) -- two from 64, where the host's share is
+    # worth hiding (128: 15.7 / 14.1 / 14.8 ms in 1 / 2 / 3);
+    # host ancestor_x: groups hide the pool's inversions
+    n_groups = 1 if (use_nem or n < 2) else (groups or ((2 if n >= 64 else 1) if dev else 3 if n >= 6 else 2))
     n_groups = max(1, min(n_groups, n))
     bounds = [n * g // n_groups for g in range(n_groups + 1)]
     glist = [list(range(bounds[g], bounds[g + 1])) for g in range(n_groups)]
