@@ -290,12 +290,14 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                tables, no parent cap, numpy's pairwise sum of E fits the
  *                wave plan)
  *   "exact_form" the exact local-optimum kernel's form (same bits): 0 auto
- *                (default: pair form while chains x pairs <= "exact_pair_waves",
- *                16384 by default, then the latency form up to
- *                "exact_lat_waves" (0), the throughput form beyond), 1 latency
- *                (one wave per optimum, two per SIMD), 2 throughput (four per
- *                SIMD), 3 pair (two waves per optimum, the objective's slots
- *                split between them; E > 1024)
+ *                (default: the latency form while chains x pairs <=
+ *                "exact_lat_waves", 32768 by default = 16 C3 chains, the
+ *                throughput form beyond; the pair form while chains x pairs <=
+ *                "exact_pair_waves", 0 by default), 1 latency (one wave per
+ *                optimum, two per SIMD, the optimum's c values held in
+ *                registers), 2 throughput (four per SIMD, c recomputed each
+ *                evaluation), 3 pair (two waves per optimum, the objective's
+ *                slots split between them; E > 1024)
  *   "anc_overlap" 1 (default): nemo_optimal_weights_w makes ancestor_x on a
  *                second stream beside eval #1 (same bits); 0 = in line */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);

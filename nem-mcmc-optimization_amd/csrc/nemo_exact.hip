@@ -26,6 +26,16 @@
 // default contraction would fuse them; the functions repeat the pragma)
 #pragma clang fp contract(off)
 
+#ifndef NEMO_EXACT_LOGPAIR
+// ExactObjective::log_pair shares the two points' log row when set; off: the
+// extra registers cost more than the lookups they save (C3, 16 chains: 1.75 vs
+// 1.50 ms per fused step; 1 chain 0.50 vs 0.46 ms; profiles/r5/r5h_logpair_ab.txt)
+#define NEMO_EXACT_LOGPAIR 0
+#endif
+#ifndef NEMO_EXACT_CCACHE
+#define NEMO_EXACT_CCACHE 1   // the latency form holds its c values in registers (ExactObjective::kCache)
+#endif
+
 namespace nemo {
 namespace {
 
@@ -332,11 +342,16 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // the same rounded operations -- so the objective reads 1.1 MB per chain
 // instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
 // starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false>
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
   const double* cp;
+  // kCache (the latency form's recompute rows, 2 waves per SIMD): the lane's
+  // c values made once per optimum (fill_cache) and held in registers through
+  // the optimiser, instead of recomputed from the a rows every evaluation --
+  // the same rc_c values, so the same bits
+  double cc[kCache ? NS : 1][kCache ? kRows : 1];
   // kRc: this lane's lv bits per slot (bit m: chain element m, bit 16: the
   // remainder), s and s (lv - 1) of both values; pad_guard: a padding
   // element's 1 + s (lo - 1) is 0 (s = 1, exp(lo) = 0), so its 0 / 0 is
@@ -386,15 +401,58 @@ struct ExactObjective {
     const double c = a / bd;
     return lb::uni(pad_guard) ? (real ? c : 0.0) : c;
   }
+  __device__ __forceinline__ void fill_cache() {
+    if (!kCache) return;
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int cu = cnt(u);
+#pragma unroll
+      for (int m = 0; m < kChain; ++m) cc[kCache ? u : 0][kCache ? m : 0] = rc_c(u, m, m < cu);
+      cc[kCache ? u : 0][kCache ? kChain : 0] = rc_c(u, kChain, rem(u) >= 0);
+    }
+  }
   __device__ __forceinline__ double cval(int u, int m, int cu) const {
+    if (kCache) return cc[kCache ? u : 0][kCache ? m : 0];
     if (kRc) return rc_c(u, m, m < cu);
     if (kPlan) return cp[(u * kRows + m) * kWave + lane];
     return m < cu ? cp[start(u) + 8 * m] : 0.0;
   }
   __device__ __forceinline__ double crem(int u, int ru) const {
+    if (kCache) return cc[kCache ? u : 0][kCache ? kChain : 0];
     if (kRc) return rc_c(u, kChain, ru >= 0);
     if (kPlan) return cp[(u * kRows + kChain) * kWave + lane];
     return ru >= 0 ? cp[ru] : 0.0;
+  }
+
+  // svml_log of the forward difference's two arguments (x and x + h: almost
+  // always one reduction row and one exponent): the second log reuses the
+  // first's row and k ln2 terms H, L when its argument shares them -- the
+  // values its own lookup would give, so the same bits -- and does its own
+  // lookup in the lanes where it crossed a switch point (a branch that is
+  // skipped when no lane did)
+  __device__ __forceinline__ void log_pair(double x0, double x1, double& y0, double& y1) const {
+#pragma clang fp contract(off)
+    if (!NEMO_EXACT_LOGPAIR) {
+      y0 = refmath::svml_log(x0, tb);
+      y1 = refmath::svml_log(x1, tb);
+      return;
+    }
+    const uint64_t b0 = refmath::as_u64(x0), b1 = refmath::as_u64(x1);
+    const uint32_t p0 = (uint32_t)(b0 >> 30) & 0x3fffff, p1 = (uint32_t)(b1 >> 30) & 0x3fffff;
+    const uint32_t bk = p0 >> 16;
+    const uint32_t thr = tb.rthr_p[bk];
+    const bool a0 = p0 >= thr;
+    const double* row = tb.lrow_p + 4 * (2 * bk + (a0 ? 1 : 0));
+    const double k = (double)(int)((b0 >> 52) & 0x7ff) + row[1];
+    const double H = refmath::fma_(k, refmath::kSvmlLn2Hi, row[2]);
+    const double L = refmath::fma_(refmath::kSvmlLn2Lo, k, row[3]);
+    y0 = refmath::svml_log_core(refmath::svml_mant(b0), row[0], H, L);
+    // exponent and bucket (bits 46..62) equal and the same side of the bucket's switch point
+    const bool same = (b0 >> 46) == (b1 >> 46) && (p1 >= thr) == a0;
+    if (__builtin_expect(same, 1))
+      y1 = refmath::svml_log_core(refmath::svml_mant(b1), row[0], H, L);
+    else
+      y1 = refmath::svml_log(x1, tb);
   }
 
   // both points of the forward difference in one pass over c (each point's
@@ -413,8 +471,8 @@ struct ExactObjective {
     // so its term is log(0 ex + 1) = +0 and a + 0 = a: a is never -0 (a log is
     // never -0, and a sum of nonzero terms rounds to +0), so no select is needed
     auto step = [&](int m, double cm) {
-      const double t0 = refmath::svml_log(cm * ex0 + 1.0, tb);
-      const double t1 = refmath::svml_log(cm * ex1 + 1.0, tb);
+      double t0, t1;
+      log_pair(cm * ex0 + 1.0, cm * ex1 + 1.0, t0, t1);
       if (m == 0) {
         a0 = t0;
         a1 = t1;
@@ -660,7 +718,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc, kLat && kRc && NEMO_EXACT_CCACHE>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -670,6 +728,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_
   obj.anc = anc[idx];
   obj.load_plan();
   setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
+  obj.fill_cache();
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
   long long c_obj = 0, c_ctl = 0, tc = ca.trace ? (long long)clock64() : 0;   // (trace: shader cycles)

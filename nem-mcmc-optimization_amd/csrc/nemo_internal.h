@@ -120,13 +120,14 @@ struct Ctx {
   // calls (nemo_exact.hip): option "exact" (1 default), available when the
   // staged model is factored and numpy's pairwise sum of E fits the wave plan
   int exact = 1;
-  // the local-optimum kernel's form: 0 auto (pair form up to exact_pair_waves
-  // optima -- measured best from 1 to 4 C3 chains, level at 16 -- then the
-  // latency form up to exact_lat_waves, the throughput form beyond), 1
+  // the local-optimum kernel's form: 0 auto (the pair form up to
+  // exact_pair_waves optima, none by default; the latency form -- its c values
+  // held in registers -- up to exact_lat_waves, 16 C3 chains, measured best
+  // from 1 to 16 chains; the throughput form beyond, best from 32), 1
   // latency, 2 throughput, 3 pair
   int exact_form = 0;
-  int exact_lat_waves = 0;
-  int exact_pair_waves = 16384;
+  int exact_lat_waves = 32768;
+  int exact_pair_waves = 0;
   bool exact_ok = false;
   double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
   double* d_xhi = nullptr;         // [S] numpy's exp(hi_j)

@@ -353,20 +353,18 @@ NEMO_RM double logaddexp(double x, double y, const TB& tb = TB{}) {
 // r < 0.75, evaluated as below.  For positive normal x (the path's logs:
 // arguments 1 + c e and 1 - w + w e^T).
 // ---------------------------------------------------------------------------
-template <class TB = ConstTabs>
-NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
+constexpr double kSvmlLn2Hi = 0x1.62e42fefa0000p-1, kSvmlLn2Lo = 0x1.cf79abc9e0000p-40;
+
+// svml_log after its reduction row: m the mantissa in [1, 2), r the row's
+// reduction point, H = fma(k, ln2_hi, T_hi) and L = fma(ln2_lo, k, T_lo) with
+// k the adjusted exponent -- each operation as the kernel does it (a caller
+// whose two arguments share a row and exponent computes H and L once)
+NEMO_RM double svml_log_core(double m, double r, double H, double L) {
   NEMO_RM_NOCONTRACT
   constexpr double C180 = 0x1.c81cd309d7c70p-4, C1c0 = -0x1.007357e93af62p-3;
   constexpr double C200 = 0x1.249229cee81efp-3, C240 = -0x1.55553fb28db06p-3;
   constexpr double C280 = 0x1.9999999cc9f5cp-3, C2c0 = -0x1.00000000c05bdp-2;
   constexpr double C300 = 0x1.5555555555466p-2, C340 = -0x1.fffffffffffc6p-2;
-  constexpr double kLn2Hi = 0x1.62e42fefa0000p-1, kLn2Lo = 0x1.cf79abc9e0000p-40;
-  const uint64_t b = as_u64(x);
-  const double m = as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-  const uint32_t p22 = (uint32_t)(b >> 30) & 0x3fffff;
-  double r, kadj, thi, tlo;
-  tb.log_row(p22, r, kadj, thi, tlo);
-  const double k = (double)(int)((b >> 52) & 0x7ff) + kadj;   // e - 1023, + 1 when r < 0.75
   const double R = fma_(r, m, -1.0);
   double p7 = fma_(R, C200, C240);
   double p1 = fma_(R, C180, C1c0);
@@ -376,14 +374,26 @@ NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
   p1 = fma_(R2, p1, p7);
   const double R4 = R2 * R2;
   p9 = fma_(R2, p9, p8);
-  const double H = fma_(k, kLn2Hi, thi);
   const double P = fma_(R4, p1, p9);
   const double S = H + R;
   const double D = S - H;
   const double E = R - D;
   const double Q = fma_(R2, P, E);
-  const double L = fma_(kLn2Lo, k, tlo);
   return S + (Q + L);
+}
+
+NEMO_RM double svml_mant(uint64_t b) { return as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull); }
+
+template <class TB = ConstTabs>
+NEMO_RM double svml_log(double x, const TB& tb = TB{}) {
+  NEMO_RM_NOCONTRACT
+  const uint64_t b = as_u64(x);
+  const double m = svml_mant(b);
+  const uint32_t p22 = (uint32_t)(b >> 30) & 0x3fffff;
+  double r, kadj, thi, tlo;
+  tb.log_row(p22, r, kadj, thi, tlo);
+  const double k = (double)(int)((b >> 52) & 0x7ff) + kadj;   // e - 1023, + 1 when r < 0.75
+  return svml_log_core(m, r, fma_(k, kSvmlLn2Hi, thi), fma_(kSvmlLn2Lo, k, tlo));
 }
 
 // ---------------------------------------------------------------------------
