@@ -253,6 +253,17 @@ done
 echo "pmc done"
 )
 
+# ---- lo_pmc: the local-optimum kernel's counters at 16 chains on the default build
+# (FETCH_SIZE, WRITE_SIZE, L2 hit / miss, VALU, waits; each set in its own pass)
+task_lo_pmc() (
+P=${PROF_DIR:-gpurun_out/lo_pmc}; mkdir -p "$P"; export TMPDIR=/tmp PYTHONUNBUFFERED=1
+for cs in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+  tag=$(echo $cs | cut -d' ' -f1)
+  timeout -s KILL 180 rocprofv3 --pmc $cs --kernel-include-regex "local_opt_exact" --output-format csv -d "$R/$P/lo_$tag" -o p -- python "$R/tools/step_probe.py" ${CHAINS:-16} > "$P/lo_$tag.log" 2>&1 || { echo "pmc $tag failed"; tail -3 "$P/lo_$tag.log"; exit 1; }
+done
+echo "lo pmc done"
+)
+
 # ---- i8l_valu: SQ_INSTS_VALU of score_i8l_kernel (C3, B = 2048) for the default build and
 # the prep-only instrumented build (libnemo_abl32.so, NEMO_I8_ABLATE=32: no tiles walked), so
 # the walk's share is the difference (DESIGN.md 3.1h's per-cell accounting)
@@ -267,6 +278,6 @@ done
 )
 
 case "$task" in
-  ab|ab_step|batch|c4_rehearsal|cform|i8l_valu|exact|exact_ab|exact_dev|exact_pmc|exact_form|exact_prof|lo|prof|small|split|step_trace) "task_$task" "$@" ;;
-  *) echo "tasks: ab ab_step batch c4_rehearsal cform i8l_valu exact exact_ab exact_dev exact_pmc exact_form exact_prof lo prof small split step_trace"; exit 2 ;;
+  ab|ab_step|batch|c4_rehearsal|cform|i8l_valu|exact|exact_ab|exact_dev|exact_pmc|exact_form|exact_prof|lo|lo_pmc|prof|small|split|step_trace) "task_$task" "$@" ;;
+  *) echo "tasks: ab ab_step batch c4_rehearsal cform i8l_valu exact exact_ab exact_dev exact_pmc exact_form exact_prof lo lo_pmc prof small split step_trace"; exit 2 ;;
 esac
