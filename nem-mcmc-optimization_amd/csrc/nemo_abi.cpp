@@ -256,7 +256,11 @@ int alloc_tables(Ctx& c) {
   HIPCHK(hipMalloc(&c.d_U, (S + 1) * E * esz));
   const size_t urows = std::max(S + 1, (size_t)std::max(nemo::factored_spad(c.S), 0));
   HIPCHK(hipMalloc((void**)&c.d_U64, (urows * E + 16) * 8));
-  HIPCHK(hipMemset(c.d_U64, 0, (urows * E + 16) * 8));
+  // on the context's stream, finished before the staging kernels run: c.stream
+  // is non-blocking, so a null-stream hipMemset is not ordered before them (it
+  // can land after the knockdown kernels wrote U, seen under a shared GPU)
+  HIPCHK(hipMemsetAsync(c.d_U64, 0, (urows * E + 16) * 8, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
   return NEMO_OK;
 }
 
@@ -761,7 +765,7 @@ int exact_reserve(Ctx& c, int nchains) {
     // the persistent form's schedule: each pair's last evaluation count (0:
     // none yet) and the hand-out order
     HIPCHK(dalloc(&c.d_xcost, nc * S * S));
-    HIPCHK(hipMemset(c.d_xcost, 0, nc * S * S * 4));
+    HIPCHK(hipMemsetAsync(c.d_xcost, 0, nc * S * S * 4, c.stream));   // stream-ordered (see alloc_tables)
     HIPCHK(dalloc(&c.d_xorder, nc * (size_t)nemo::pairs_per_chain(c.S, 0)));
     HIPCHK(dalloc(&c.d_xhist, nc * 64));
     c.cap_xorder = nc * (size_t)nemo::pairs_per_chain(c.S, 0);
@@ -784,7 +788,7 @@ int exact_reserve(Ctx& c, int nchains) {
       HIPCHK(dalloc(&c.d_xa, need));
       // positions without an element stay 0 (the order-weight launch writes
       // only real elements): their c is 0 / b = 0, as in a stored row
-      HIPCHK(hipMemset(c.d_xa, 0, need * 8));
+      HIPCHK(hipMemsetAsync(c.d_xa, 0, need * 8, c.stream));
       c.cap_xa = need;
     }
   } else {

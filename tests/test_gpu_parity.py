@@ -804,6 +804,39 @@ def test_stage_knockdown_rejects_bad_input():
         Engine.from_knockdown(m.observed_knockdown_mat, m.A, 30.0, dtype="f32")
 
 
+def test_staging_while_the_gpu_is_busy():
+    """Staging from D zero-fills U's padding before the knockdown kernels write
+    U, on the context's (non-blocking) stream: a null-stream fill is not
+    ordered before them and landed after them when another process shared
+    the GPU (garbage scores in the N = 2 rehearsal).  Stage C2 engines while a
+    128-chain C3 step runs on another context: every one scores the golden
+    bits."""
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m3 = generator.config_nem("C3")
+    busy = Engine.for_nem(m3)
+    rng = np.random.default_rng(5)
+    n = 128
+    pos3 = np.array([np.argsort(rng.permutation(64)) for _ in range(n)], dtype=np.int32)
+    call = busy.bind_optimal_weights_w(pos3, rng.uniform(-3, 3, (n, 64, 64)), SIG0, SIG1, want_prep=False)
+    m2 = generator.config_nem("C2")
+    perm = rng.permutation(16)
+    pos = np.argsort(perm)[None].astype(np.int32)
+    w01 = expit(rng.uniform(-3, 3, (1, 16, 16)))
+    ref = no.order_score(m2.U, m2.get_score_tensor(), perm, w01[0])
+    try:
+        for _ in range(3):
+            call.ended = False
+            call.begin()
+            engs = [Engine.for_nem(m2) for _ in range(4)]
+            call.end()
+            for e in engs:
+                assert abs(e.score(pos, w01)[0] - ref) <= 1e-9
+                e.close()
+    finally:
+        call.end()
+        busy.close()
+
+
 def test_order_weights_per_sampler_on_shared_engine():
     """order_weights / calculate_local_optimum read THIS sampler's eval #1
     (nem_order_mcmc.py:181-182, 160-170), also when other samplers share the
