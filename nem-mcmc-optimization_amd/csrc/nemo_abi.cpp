@@ -373,9 +373,6 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     int rc2 = nemo_reserve(ctx, nb, 0);
     if (rc2) return rc2;
   }
-  // the tables above went up by null-stream copies: done before any kernel on
-  // the (non-blocking) context stream may read them
-  HIPCHK(hipDeviceSynchronize());
   c.staged = true;
   return NEMO_OK;
 }
