@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -65,6 +66,19 @@ int fail(int code, const char* fmt, ...) {
       return fail(NEMO_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
   } while (0)
 
+// One process-wide lock around graph capture and the calls that allocate,
+// free, or use the legacy stream (staging, reserve, context create / destroy,
+// the probes): a step captured on one engine's step thread and such a call on
+// another engine in another thread must not overlap -- HIP refuses a
+// legacy-stream operation while a stream captures ("would make the legacy
+// stream depend on a capturing blocking stream"), and the error then sticks
+// to the next launch (tests/test_gpu_parity.py::test_staging_while_the_gpu_is_busy)
+std::recursive_mutex& api_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
+#define NEMO_API_LOCK std::lock_guard<std::recursive_mutex> nemo_api_lock_(api_mutex())
+
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
   if (*p) {
@@ -111,6 +125,7 @@ int nemo_device_count(int* count) {
 }
 
 int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out) {
+  NEMO_API_LOCK;
   if (!out) return fail(NEMO_ERR_ARG, "null out");
   *out = nullptr;
   if (num_s < 2 || num_s > nemo::kMaxS)
@@ -141,6 +156,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
   // every queued step still runs (its caller's buffers are written), then the
   // step thread ends; steps not collected with _end are dropped
   if (ctx->steps) ctx->steps->shutdown();
+  NEMO_API_LOCK;
   Ctx& c = ctx->c;
   // teardown is best effort: a failure here has no caller left to report to
   (void)hipSetDevice(c.device);
@@ -172,6 +188,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
 }
 
 int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
+  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (max_batch < 0 || max_chains < 0) return fail(NEMO_ERR_ARG, "negative capacity");
@@ -223,6 +240,7 @@ namespace {
 int step_stage(Ctx& c, int slot, size_t bytes) {
   if (!c.step_done[slot]) HIPCHK(hipEventCreateWithFlags(&c.step_done[slot], hipEventDisableTiming));
   if (bytes <= c.h_stage_bytes[slot] && bytes <= c.d_step_bytes[slot]) return NEMO_OK;
+  NEMO_API_LOCK;
   ++c.graph_epoch;
   HIPCHK(hipStreamSynchronize(c.stream));
   if (c.h_stage[slot]) HIPCHK(hipHostFree(c.h_stage[slot]));
@@ -382,6 +400,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
 extern "C" {
 
 int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
+  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!U || !T) return fail(NEMO_ERR_ARG, "null table");
@@ -436,6 +455,7 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
 }
 
 int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
+  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!D) return fail(NEMO_ERR_ARG, "null knockdown matrix");
@@ -757,6 +777,7 @@ bool step_exact(const Ctx& c, int) { return use_factored(c) && c.exact && nemo::
 // rows (d_xcbuf, chains x pairs x plan: 35 MB per chain at C3).  A failed
 // allocation is the call's error -- the step never drops to other arithmetic
 int exact_reserve(Ctx& c, int nchains) {
+  NEMO_API_LOCK;
   const size_t S = c.S, E = c.E, plan = nemo::exact_plan_doubles(c), nc = (size_t)std::max(nchains, 1);
   if (!c.d_xcells2 || c.cap_xcells2 < nc) {
     ++c.graph_epoch;
@@ -953,6 +974,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if (from_w && !nemo::ancestor_supported(c))
     return fail(NEMO_ERR_ARG, "S=%d > 64: ancestor_x on the device covers S <= 64 (give W~ and ancestor_x)", c.S);
   if (from_w && c.anc_overlap && !c.stream2) {  // created before any capture
+    NEMO_API_LOCK;
     HIPCHK(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c.ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c.ev_join, hipEventDisableTiming));
@@ -1020,6 +1042,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
           g.sig0 == sig0 && g.sig1 == sig1 && g.from_w == from_w && g.want_prep == want_prep)
         sg = &g;
     if (!sg) {  // capture once
+      NEMO_API_LOCK;
       Ctx::StepGraph& g = c.step_graph[c.step_graph_next];
       c.step_graph_next = (c.step_graph_next + 1) % Ctx::kStepGraphs;
       if (g.exec) {
@@ -1237,6 +1260,7 @@ int nemo_ancestor_dev(nemo_ctx* ctx, int nchains, const int32_t* d_pos, const do
 }
 
 int nemo_fetch_exact_trace(nemo_ctx* ctx, int* n, long long* out) {
+  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!n) return fail(NEMO_ERR_ARG, "null n");
@@ -1341,6 +1365,7 @@ int nemo_gamma_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const double*
 }
 
 int nemo_inverse_ancestral(nemo_ctx* ctx, int nprob, const int32_t* pos, const double* w, double* out) {
+  NEMO_API_LOCK;
   int rc = methods_prologue(ctx, nprob, pos, w);
   if (rc || nprob == 0) return rc;
   if (!out) return fail(NEMO_ERR_ARG, "null host pointer");
@@ -1524,6 +1549,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
 }
 
 int nemo_refmath_probe(int fn, int n, const double* x, const double* y, double* out) {
+  NEMO_API_LOCK;
   if (n < 0 || fn < 0 || fn > 8 || (n > 0 && (!x || !out || ((fn == 3 || fn == 7) && !y))))
     return fail(NEMO_ERR_ARG, "fn=%d n=%d / null pointer", fn, n);
   if (n == 0) return NEMO_OK;
@@ -1598,6 +1624,7 @@ const char* nemo_build_id(void) {
 // timing
 // ---------------------------------------------------------------------------
 int nemo_timing_enable(nemo_ctx* ctx, int enable) {
+  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   Ctx& c = ctx->c;

@@ -827,7 +827,7 @@ def test_staging_while_the_gpu_is_busy():
         for _ in range(3):
             call.ended = False
             call.begin()
-            engs = [Engine.for_nem(m2) for _ in range(4)]
+            engs = [Engine.from_knockdown(m2.observed_knockdown_mat, m2.A, m2.B) for _ in range(4)]
             call.end()
             for e in engs:
                 assert abs(e.score(pos, w01)[0] - ref) <= 1e-9
