@@ -721,14 +721,32 @@ def main():
         # median reported
         n_it = 30
         e2e = {}
+        # the fused calls the sampler itself makes, timed in place (its own
+        # inputs: the step's cost depends on them), so the host's share is the
+        # run's wall time minus these
+        from nemo import engine as nengine
+        call_run = nengine._OptimalWeightsWCall.run
+        in_call = []
+
+        def timed_run(self):
+            t0 = time.perf_counter()
+            call_run(self)
+            in_call[-1] += time.perf_counter() - t0
+
         for tag, pl, reps in (("device", None, 3), ("pool", pool, 1)):
             ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pl).run(2)
             walls = []
             for _ in range(reps):
                 cb = ChainBatch(m, [order0] * nch, seeds=seeds, engine=eng, on_fail="continue", inv_pool=pl)
-                t0 = time.perf_counter()
-                cb.run(n_it)
-                walls.append(time.perf_counter() - t0)
+                if pl is None:
+                    in_call.append(0.0)
+                    nengine._OptimalWeightsWCall.run = timed_run
+                try:
+                    t0 = time.perf_counter()
+                    cb.run(n_it)
+                    walls.append(time.perf_counter() - t0)
+                finally:
+                    nengine._OptimalWeightsWCall.run = call_run
             e2e[tag] = (float(np.median(walls)), cb.best_scores, walls)
         # the same sampler with the fast kernels (the host's share of a step)
         eng.set_option("exact", 0)
@@ -745,6 +763,11 @@ def main():
             "ms_per_step_runs": [1e3 * w / n_it for w in e2e["device"][2]],
             "chain_steps_per_s": nch * n_it / dt,
             "over_fused_step": (dt / n_it) / fs,
+            # the sampler's own fused calls (its inputs), timed in place: the
+            # step's device + transfer share and the host's share of the wall
+            "fused_calls_ms_per_step": 1e3 * float(np.median(in_call)) / n_it,
+            "host_ms_per_step": 1e3 * (dt - float(np.median(in_call))) / n_it,
+            "over_own_fused_calls": dt / float(np.median(in_call)) if in_call and min(in_call) > 0 else None,
             "includes": "ChainBatch.run: proposals, reset quirks and accept per chain on the host + the fused "
                         "device step from W (W~ and ancestor_x on the device, in scipy's bits)",
             "ms_per_step_host_pool": 1e3 * e2e["pool"][0] / n_it,
