@@ -16,6 +16,9 @@
  *     before return); *_dev calls take device pointers and only enqueue work on
  *     the given stream (hipStream_t passed as void*; NULL = HIP's null stream);
  *   - one context per (device, model); calls on one context must not overlap.
+ *     Different contexts may be driven from different threads: graph capture
+ *     and the calls that allocate or use the legacy stream (create, destroy,
+ *     stage, reserve, the probes) serialise on one process-wide lock.
  *
  * Layouts (row-major, C order):
  *   T    [S][S][E]  score table, T[i][j][e]: child i, candidate parent j
