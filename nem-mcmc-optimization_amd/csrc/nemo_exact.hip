@@ -32,6 +32,9 @@
 // 1.50 ms per fused step; 1 chain 0.50 vs 0.46 ms; profiles/r5/r5h_logpair_ab.txt)
 #define NEMO_EXACT_LOGPAIR 0
 #endif
+#ifndef NEMO_EXACT_TPUT_WAVES
+#define NEMO_EXACT_TPUT_WAVES 4   // the throughput form's waves per SIMD (its register budget)
+#endif
 #ifndef NEMO_EXACT_CCACHE
 #define NEMO_EXACT_CCACHE 1   // the latency form holds its c values in registers (ExactObjective::kCache)
 #endif
@@ -678,7 +681,7 @@ __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E,
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
 template <int NS, bool kLat, bool kRc>
 __global__ __launch_bounds__(kExactWaves * kWave)
-__attribute__((amdgpu_waves_per_eu(kLat ? 2 : 4, kLat ? 2 : 4))) void local_opt_exact_kernel(
+__attribute__((amdgpu_waves_per_eu(kLat ? 2 : NEMO_EXACT_TPUT_WAVES, kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
