@@ -75,7 +75,11 @@ int nemo_device_count(int* count);
 int nemo_ctx_create(int device, int num_s, int num_e, int dtype, nemo_ctx** out);
 void nemo_ctx_destroy(nemo_ctx* ctx);
 /* grow per-batch scratch so *_dev calls with up to max_batch evaluations
- * (and max_chains chains for nemo_optimal_weights_dev) never allocate */
+ * (and max_chains chains for nemo_optimal_weights_dev) never allocate: with a
+ * model staged (before or after this call) that covers the exact step's
+ * buffers as well, so such a _dev call only enqueues and may be captured into
+ * the caller's graph.  Without the reservation the first _dev call with more
+ * chains allocates and synchronises the context's stream (not capturable). */
 int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains);
 
 /* ---- A1/A2: stage the model once (nem.py:25-64 outputs) ---------------- */

@@ -108,6 +108,9 @@ int check_pos(const int32_t* pos, int batch, int S) {
 // stream (torch's default stream), as in the HIP API itself
 hipStream_t pick(nemo_ctx*, void* stream) { return (hipStream_t)stream; }
 
+bool step_exact(const Ctx& c, int);
+int exact_reserve(Ctx& c, int nchains);
+
 }  // namespace
 
 extern "C" {
@@ -228,6 +231,9 @@ int nemo_reserve(nemo_ctx* ctx, int max_batch, int max_chains) {
     HIPCHK(dalloc(&c.d_xcs, 2 * nc * E));
     c.cap_chains = nc;
   }
+  // the exact step's own buffers too, so nemo_optimal_weights_dev never
+  // allocates (or synchronises) once this returned -- a caller may capture it
+  if (max_chains > 0 && c.staged && step_exact(c, 0)) return exact_reserve(c, nc);
   return NEMO_OK;
 }
 
@@ -392,6 +398,8 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     if (rc2) return rc2;
   }
   c.staged = true;
+  // a chain reservation made before this staging covers the exact step too
+  if (c.cap_chains > 0 && step_exact(c, 0)) return exact_reserve(c, c.cap_chains);
   return NEMO_OK;
 }
 
@@ -779,7 +787,9 @@ bool step_exact(const Ctx& c, int) { return use_factored(c) && c.exact && nemo::
 int exact_reserve(Ctx& c, int nchains) {
   NEMO_API_LOCK;
   const size_t S = c.S, E = c.E, plan = nemo::exact_plan_doubles(c), nc = (size_t)std::max(nchains, 1);
+  bool grew = false;
   if (!c.d_xcells2 || c.cap_xcells2 < nc) {
+    grew = true;
     ++c.graph_epoch;
     HIPCHK(hipStreamSynchronize(c.stream));
     HIPCHK(dalloc(&c.d_xcells2, nc * (S + 1) * E));
@@ -811,6 +821,7 @@ int exact_reserve(Ctx& c, int nchains) {
       // only real elements): their c is 0 / b = 0, as in a stored row
       HIPCHK(hipMemsetAsync(c.d_xa, 0, need * 8, c.stream));
       c.cap_xa = need;
+      grew = true;
     }
   } else {
     const size_t need = nc * (size_t)nemo::pairs_per_chain(c.S, 0) * plan;
@@ -821,6 +832,11 @@ int exact_reserve(Ctx& c, int nchains) {
       c.cap_xcbuf = need;
     }
   }
+  // the zero fills above ran on c.stream (non-blocking): finish them before
+  // any other stream -- the caller's of a _dev call, the null stream included
+  // -- queues the step that reads them (a late d_xa fill would wipe real a
+  // rows; unfilled d_xcost would give sched_bucket negative costs)
+  if (grew) HIPCHK(hipStreamSynchronize(c.stream));
   return NEMO_OK;
 }
 
@@ -937,9 +953,10 @@ namespace {
 // (npart: the most any score kernel writes per evaluation)
 struct StepLayout {
   size_t o_pos, o_w01, o_anc, o_wn, o_inf, o_ll1, o_lld, o_flag, o_part, total;
-  StepLayout(size_t S, size_t n, size_t npart) {
+  // from_w: the W segment leads the slot; the W~ / ancestor_x calls have none
+  StepLayout(size_t S, size_t n, size_t npart, bool from_w) {
     auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    o_pos = up(n * S * S * 8);
+    o_pos = from_w ? up(n * S * S * 8) : 0;
     o_w01 = o_pos + up(n * S * 4);
     o_anc = o_w01 + up(n * S * S * 8);
     o_wn = o_anc + up(n * S * S * 8);
@@ -984,7 +1001,7 @@ static int step_start(nemo_ctx* ctx, int slot, int nchains, const int32_t* pos, 
   if (cap >= 0 && step_exact(c, cap) && (rc = exact_reserve(c, nchains))) return rc;
   const size_t S = c.S, n = nchains;
   hipStream_t st = c.stream;
-  const StepLayout L(S, n, step_npart(c));
+  const StepLayout L(S, n, step_npart(c), from_w);
   if ((rc = step_stage(c, slot, L.total))) return rc;
   char* hs = (char*)c.h_stage[slot];
   char* ds = (char*)c.d_step[slot];
@@ -1109,7 +1126,7 @@ static int step_finish(nemo_ctx* ctx, int slot, int nchains, double* w_new, doub
   Ctx& c = ctx->c;
   if (nchains == 0) return NEMO_OK;
   const size_t S = c.S, n = nchains;
-  const StepLayout L(S, n, step_npart(c));
+  const StepLayout L(S, n, step_npart(c), from_w);
   HIPCHK(hipEventSynchronize(c.step_done[slot]));
   const char* hs = (const char*)c.h_stage[slot];
   if (from_w) {
@@ -1434,8 +1451,9 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "exact_form") == 0) {
-    if (value < 0 || value > 3)
-      return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair)", value);
+    if (value < 0 || value > 4)
+      return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair, 4 cached throughput)",
+                  value);
     ctx->c.exact_form = value;
     return NEMO_OK;
   }

@@ -28,7 +28,7 @@
 //  * np.clip (numpy 2.2's SIMD loop: x < lo ? lo : x, then > hi ? hi : x, so
 //    -0.0 stays -0.0) of inv - I.
 // The restatement was derived against the library's own kernels on the host
-// (tools/lapack_restate_check.c: 0 differing bits for n = 1..128 getrf and
+// (tests/host/lapack_check.c: 0 differing bits for n = 1..128 getrf and
 // n = 1..64 getri) and the device build is compared with scipy.linalg.inv by
 // tests/test_gpu_ancestor.py.
 //

@@ -35,6 +35,9 @@
 #ifndef NEMO_EXACT_TPUT_WAVES
 #define NEMO_EXACT_TPUT_WAVES 4   // the throughput form's waves per SIMD (its register budget)
 #endif
+#ifndef NEMO_EXACT_CT_WAVES
+#define NEMO_EXACT_CT_WAVES 3   // the cached throughput form's waves per SIMD (form 4)
+#endif
 #ifndef NEMO_EXACT_CCACHE
 #define NEMO_EXACT_CCACHE 1   // the latency form holds its c values in registers (ExactObjective::kCache)
 #endif
@@ -679,9 +682,12 @@ __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E,
 
 // one wave per (chain, permissible pair), kExactWaves per block; then the
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
-template <int NS, bool kLat, bool kRc>
+// kCt (form 4, the cached throughput form): the throughput form's objective
+// loop on the latency form's register c cache, at NEMO_EXACT_CT_WAVES per SIMD
+template <int NS, bool kLat, bool kRc, bool kCt = false>
 __global__ __launch_bounds__(kExactWaves * kWave)
-__attribute__((amdgpu_waves_per_eu(kLat ? 2 : NEMO_EXACT_TPUT_WAVES, kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
+__attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES,
+                                   kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
@@ -721,7 +727,7 @@ __attribute__((amdgpu_waves_per_eu(kLat ? 2 : NEMO_EXACT_TPUT_WAVES, kLat ? 2 : 
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc, kLat && kRc && NEMO_EXACT_CCACHE>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -1120,6 +1126,7 @@ template <int NS, bool kRc>
 int lo_resident(int form) {
   if (form == 3) return resident_blocks<local_opt_exact_pair_kernel<NS, kRc>>(2 * kWave);
   if (form == 1) return resident_blocks<local_opt_exact_kernel<NS, true, kRc>>(kExactWaves * kWave);
+  if (form == 4) return resident_blocks<local_opt_exact_kernel<NS, false, kRc, true>>(kExactWaves * kWave);
   return resident_blocks<local_opt_exact_kernel<NS, false, kRc>>(kExactWaves * kWave);
 }
 
@@ -1134,6 +1141,10 @@ void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else if (form == 1)
     local_opt_exact_kernel<NS, true, kRc><<<grid, kExactWaves * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+  else if (form == 4)
+    local_opt_exact_kernel<NS, false, kRc, true><<<grid, kExactWaves * kWave, 0, st>>>(
         a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else

@@ -178,8 +178,11 @@ class Engine:
     @property
     def device_ancestor(self) -> bool:
         """True when the fused step can start from W itself: W~ and
-        ancestor_x made on the device in scipy's bits (S <= 64)."""
-        return self.S <= 64
+        ancestor_x made on the device in scipy's bits (S <= 64).  The device
+        restates scipy's OpenBLAS with its SkylakeX kernels:
+        on a host whose scipy selects other kernels, its own inv gives other
+        bits, so the sampler inverts on the host there (with a warning)."""
+        return self.S <= 64 and host_blas_is_restated()
 
     def optimal_weights_w(self, pos, w, sig0, sig1, cap: int = 0, raise_on_fail=True, want_prep=True):
         """``optimal_weights`` from the weights themselves: the device makes
@@ -294,6 +297,46 @@ class Engine:
         n = C.c_int32(0)
         check(_lib.load().nemo_timing_read(self._ctx, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+
+_HOST_BLAS = None
+
+
+def host_blas_arch():
+    """The architecture of the OpenBLAS kernels scipy.linalg runs on this
+    host (threadpoolctl), or None when it cannot be told."""
+    global _HOST_BLAS
+    if _HOST_BLAS is None:
+        arch = ""
+        try:
+            import scipy.linalg  # noqa: F401  (loads its OpenBLAS)
+            from threadpoolctl import threadpool_info
+            for p in threadpool_info():
+                if p.get("internal_api") == "openblas" and "scipy" in p.get("filepath", ""):
+                    arch = p.get("architecture") or ""
+                    break
+        except Exception:  # threadpoolctl absent: cannot tell
+            arch = ""
+        _HOST_BLAS = arch
+    return _HOST_BLAS or None
+
+
+def host_blas_is_restated() -> bool:
+    """True when scipy's OpenBLAS on this host runs the SkylakeX kernels the
+    device's getrf / getri restate (csrc/nemo_ancestor.hip), or when the host
+    cannot be told (then with a warning: the device's bits are SkylakeX's)."""
+    import warnings
+    arch = host_blas_arch()
+    if arch == "SkylakeX":
+        return True
+    if arch is None:
+        warnings.warn("cannot tell which OpenBLAS kernels scipy runs on this host (threadpoolctl): the device's "
+                      "ancestor_x has the bits of scipy's SkylakeX kernels", ExactArithmeticWarning, stacklevel=3)
+        return True
+    warnings.warn(f"scipy's OpenBLAS runs {arch} kernels on this host, not the SkylakeX kernels the device's "
+                  "ancestor_x restates: ancestor_x is made on the host (scipy.linalg.inv)",
+                  ExactArithmeticWarning, stacklevel=3)
+    return False
 
 
 _LSE_ENGINES = {}

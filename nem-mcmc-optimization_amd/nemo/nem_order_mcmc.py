@@ -245,8 +245,20 @@ class NEMOrderMCMC:
             if self.engine.device_ancestor:
                 # W~ = expit on the permissible entries and ancestor_x (:98-103,
                 # :185) made on the device, in scipy's bits
-                w01, anc, w_new, ll1, lld, info = self.engine.optimal_weights_w(
-                    pos[None, :], w[None], SIG0, SIG1, cap=self.cap, raise_on_fail=init)
+                try:
+                    w01, anc, w_new, ll1, lld, info = self.engine.optimal_weights_w(
+                        pos[None, :], w[None], SIG0, SIG1, cap=self.cap, raise_on_fail=init)
+                except Exception as e:
+                    # the reference sets order_weights (:182) before inv can
+                    # raise and ancestor_x (:185) before a local optimum can:
+                    # both follow this step's W (made from it when read); an
+                    # error of inv itself (LinAlgError / ValueError) leaves the
+                    # previous ancestor_x, as the reference's assignment never ran
+                    wc = np.array(w, dtype=np.float64, copy=True)
+                    if not isinstance(e, (np.linalg.LinAlgError, ValueError)):
+                        self._set_ancestor_src(pos.copy(), wc)
+                    self._set_eval1(pos.copy(), None, wc)
+                    raise
                 w01, self.ancestor_x = w01[0], anc[0]
             else:
                 w01 = expit(w)

@@ -1067,3 +1067,56 @@ def test_fused_step_host_summed_ll_dag_equals_device_sum(n, cap):
     assert np.array_equal(d2.cpu().numpy(), lld)
     assert np.array_equal(d1.cpu().numpy(), ll1)
     eng.close()
+
+
+@pytest.mark.parametrize("capture", [False, True])
+def test_fused_step_dev_first_call_on_a_side_stream(capture):
+    """nemo_optimal_weights_dev as the first step call of a fresh engine, on a
+    non-null stream: nemo_reserve covers the exact step's buffers (zero-filled
+    and finished on the context's stream before it returns), so the call only
+    enqueues -- it may even be captured into the caller's graph -- and gives
+    the host path's bits (the fills used to race the step)."""
+    import ctypes as C
+    import torch
+    from nemo import _lib
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m = generator.synthetic_nem(64, 2000, 0)
+    n = 3
+    rng = np.random.default_rng(7)
+    pos = np.array([rng.permutation(64) for _ in range(n)], dtype=np.int32)
+    w = rng.uniform(-3, 3, (n, 64, 64))
+    anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
+    host = Engine.from_knockdown(m.observed_knockdown_mat, m.A, m.B)
+    w_new, ll1, lld, info = host.optimal_weights(pos, expit(w), anc, w, SIG0, SIG1, raise_on_fail=False)
+    host.close()
+    eng = Engine.from_knockdown(m.observed_knockdown_mat, m.A, m.B)
+    eng.reserve(n, n)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+        dp, dw, da = dev(pos), dev(expit(w)), dev(anc)
+        dn = torch.zeros((n, 64, 64), dtype=torch.float64, device="cuda")
+        d1 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        d2 = torch.zeros(n, dtype=torch.float64, device="cuda")
+        di = torch.zeros((n, 64, 64), dtype=torch.int32, device="cuda")
+    side.synchronize()
+    args = (eng._ctx, n, C.c_void_p(dp.data_ptr()), C.c_void_p(dw.data_ptr()), C.c_void_p(da.data_ptr()),
+            SIG0, SIG1, 0, C.c_void_p(dn.data_ptr()), C.c_void_p(d1.data_ptr()), C.c_void_p(d2.data_ptr()),
+            C.c_void_p(di.data_ptr()))
+    lib = _lib.load()
+    if capture:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            rc = lib.nemo_optimal_weights_dev(*args, C.c_void_p(side.cuda_stream))
+        assert rc == 0, lib.nemo_last_error()
+        g.replay()
+    else:
+        rc = lib.nemo_optimal_weights_dev(*args, C.c_void_p(side.cuda_stream))
+        assert rc == 0, lib.nemo_last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(d1.cpu().numpy(), ll1)
+    assert np.array_equal(d2.cpu().numpy(), lld)
+    mask = info != -1
+    assert np.array_equal(di.cpu().numpy(), info)
+    assert np.array_equal(dn.cpu().numpy()[mask], w_new[mask])
+    eng.close()
