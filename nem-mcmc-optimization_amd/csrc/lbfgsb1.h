@@ -58,9 +58,17 @@ NEMO_LB bool uni(bool b) {
   return b;
 #endif
 }
+// H (the dual form, nemo_exact.hip): the condition is uniform within each
+// half of the wave -- two optima's controls share the wave -- so it is a
+// divergent branch (exec masks), not the first lane's decision
+template <bool H>
+NEMO_LB bool uniH(bool b) {
+  return H ? b : uni(b);
+}
 NEMO_LB double dmin(double a, double b) { return a < b ? a : b; }
 
 // MINPACK-2 dcstep: safeguarded step and interval update.
+template <bool H = false>
 NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy,
                               double& dy, double& stp, double fp, double dp, bool& brackt,
                               double stpmin, double stpmax) {
@@ -71,7 +79,7 @@ NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy
   // this (and every test of sgnd is then false, as with the quotient)
   const double sgnd = (dx != 0.0 && fabs(dx) < __builtin_inf()) ? (dx > 0.0 ? dp : -dp) : __builtin_nan("");
   double stpf;
-  if (uni(fp > fx)) {
+  if (uniH<H>(fp > fx)) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -84,7 +92,7 @@ NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy
     const double stpq = stx + ((dx / ((fx - fp) / (stp - stx) + dx)) / 2.0) * (stp - stx);
     stpf = (fabs(stpc - stx) < fabs(stpq - stx)) ? stpc : stpc + (stpq - stpc) / 2.0;
     brackt = true;
-  } else if (uni(sgnd < 0.0)) {
+  } else if (uniH<H>(sgnd < 0.0)) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -97,7 +105,7 @@ NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy
     const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
     stpf = (fabs(stpc - stp) > fabs(stpq - stp)) ? stpc : stpq;
     brackt = true;
-  } else if (uni(fabs(dp) < fabs(dx))) {
+  } else if (uniH<H>(fabs(dp) < fabs(dx))) {
     const double theta = 3.0 * (fx - fp) / (stp - stx) + dx + dp;
     const double s = dmax(dmax(fabs(theta), fabs(dx)), fabs(dp));
     const double ts = theta / s;
@@ -111,7 +119,7 @@ NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy
     else if (stp > stx) stpc = stpmax;
     else stpc = stpmin;
     const double stpq = stp + (dp / (dp - dx)) * (stx - stp);
-    if (uni(brackt)) {
+    if (uniH<H>(brackt)) {
       stpf = (fabs(stpc - stp) < fabs(stpq - stp)) ? stpc : stpq;
       if (stp > stx) stpf = dmin(stp + 0.66 * (sty - stp), stpf);
       else stpf = dmax(stp + 0.66 * (sty - stp), stpf);
@@ -121,7 +129,7 @@ NEMO_LB void dcstep(double& stx, double& fx, double& dx, double& sty, double& fy
       stpf = dmax(stpmin, stpf);
     }
   } else {
-    if (uni(brackt)) {
+    if (uniH<H>(brackt)) {
       const double theta = 3.0 * (fp - fy) / (sty - stp) + dy + dp;
       const double s = dmax(dmax(fabs(theta), fabs(dy)), fabs(dp));
       const double ts = theta / s;
@@ -163,9 +171,10 @@ struct Dcsrch {
   double stpmax = kStpMax;  // lnsrlb's stpmx (1e10 unbounded; from the bounds otherwise)
 
   // returns false on ERROR (initial derivative not negative)
+  template <bool H = false>
   NEMO_LB bool start(double stp, double f, double g) {
 #pragma clang fp contract(off)
-    if (uni(!(g < 0.0))) return false;
+    if (uniH<H>(!(g < 0.0))) return false;
     brackt = false;
     stage = 1;
     finit = f;
@@ -182,6 +191,7 @@ struct Dcsrch {
 
   // one dcsrch call with (f, g) at stp; returns 0 = FG (evaluate new stp),
   // 1 = CONV, 2 = WARN
+  template <bool H = false>
   NEMO_LB int step(double& stp, double f, double g) {
 #pragma clang fp contract(off)
     const double stpmin = 0.0;
@@ -193,12 +203,12 @@ struct Dcsrch {
     if (stp == stpmax && f <= ftest && g <= gtest) task = 2;
     if (stp == stpmin && (f > ftest || g >= gtest)) task = 2;
     if (f <= ftest && fabs(g) <= kGtolLs * (-ginit)) task = 1;
-    if (uni(task != 0)) return task;
+    if (uniH<H>(task != 0)) return task;
     // one dcstep call site on locals (keeps the state in registers): the
     // modified function psi is used in stage 1 when f fell but not enough
     const bool modified = stage == 1 && f <= fx && f > ftest;
     double sx = stx, sy = sty, fxl = fx, gxl = gx, fyl = fy, gyl = gy, fp = f, gp = g;
-    if (uni(modified)) {
+    if (uniH<H>(modified)) {
       fp = f - stp * gtest;
       fxl = fx - stx * gtest;
       fyl = fy - sty * gtest;
@@ -206,10 +216,10 @@ struct Dcsrch {
       gxl = gx - gtest;
       gyl = gy - gtest;
     }
-    dcstep(sx, fxl, gxl, sy, fyl, gyl, stp, fp, gp, brackt, stmin, stmax);
+    dcstep<H>(sx, fxl, gxl, sy, fyl, gyl, stp, fp, gp, brackt, stmin, stmax);
     stx = sx;
     sty = sy;
-    if (uni(modified)) {
+    if (uniH<H>(modified)) {
       fx = fxl + stx * gtest;
       fy = fyl + sty * gtest;
       gx = gxl + gtest;
@@ -217,7 +227,7 @@ struct Dcsrch {
     } else {
       fx = fxl; fy = fyl; gx = gxl; gy = gyl;
     }
-    if (uni(brackt)) {
+    if (uniH<H>(brackt)) {
       if (fabs(sty - stx) >= 0.66 * width1) stp = stx + 0.5 * (sty - stx);
       width1 = width;
       width = fabs(sty - stx);

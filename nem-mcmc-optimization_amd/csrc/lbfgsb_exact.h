@@ -38,6 +38,7 @@ namespace lbx {
 using lb::dmax;
 using lb::dmin;
 using lb::uni;
+using lb::uniH;
 
 constexpr int kM = 10;          // scipy's default memory
 constexpr int kLdN = 2 * kM;    // WN's leading dimension (m2)
@@ -88,9 +89,11 @@ NEMO_LB double ob_ddot(int n, const double* x, const double* y) {
 struct Lanes {
   int id, n;
 };
+// H: the dual form's half wave (lanes 32 h .. 32 h + 31 run optimum h)
+template <bool H = false>
 NEMO_LB Lanes lanes() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return Lanes{(int)__lane_id(), 64};
+  return H ? Lanes{(int)__lane_id() & 31, 32} : Lanes{(int)__lane_id(), 64};
 #else
   return Lanes{0, 1};
 #endif
@@ -109,6 +112,18 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// lane l of this lane's group (H: of its half) to every lane of the group.
+// H: l is uniform within each half but may differ between them (a loop from
+// 2 col - 1 down, col + j), so each half's l is read from the half's first
+// lane and each half's value from its own lane (readlane takes a uniform
+// lane number: one for both halves would serve the first active half only)
+template <bool H>
+__device__ __forceinline__ double bcast(double v, int l) {
+  if (!H) return readlane_d(v, l);
+  const int la = __builtin_amdgcn_readlane(l, 0) & 31, lb = __builtin_amdgcn_readlane(l, 32) & 31;
+  const double a = readlane_d(v, la), b = readlane_d(v, 32 + lb);
+  return (__lane_id() & 32) ? b : a;
 }
 #endif
 
@@ -175,12 +190,13 @@ NEMO_LB double ob_gemv_t_m1_col(int m, int n, int c, const double* a, int lda, c
 // OpenBLAS dpotrf('U') for n <= 16 (potf2_U); returns info (0 or j + 1).
 // Row j's update (dgemv_t) and scaling by 1 / ajj: one column per lane.
 #if !defined(__HIP_DEVICE_COMPILE__)
+template <bool H = false>
 NEMO_LB int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 #pragma clang fp contract(off)
   for (int j = 0; j < n; ++j) {
     double* cj = a + (long)j * lda;
     double ajj = cj[j] - ob_ddot(j, cj, cj);
-    if (uni(ajj <= 0.0)) {   // potf2: a NaN goes on to the square root
+    if (uniH<H>(ajj <= 0.0)) {   // potf2: a NaN goes on to the square root
       cj[j] = ajj;
       return j + 1;
     }
@@ -204,6 +220,7 @@ NEMO_LB int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 // On the wave lane c owns column c (n <= 16): it also accumulates ddot(c,
 // A(:, c), A(:, c)) -- for n < 16 a chain in row order -- as the rows of its
 // column become final, so step j starts from its diagonal at once.
+template <bool H = false>
 __device__ __forceinline__ int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 #pragma clang fp contract(off)
   const int ln = L.id;
@@ -212,8 +229,8 @@ __device__ __forceinline__ int ob_potrf_u(int n, double* a, int lda, Lanes L) {
   for (int j = 0; j < n; ++j) {
     double* cj = a + (long)j * lda;
     double ajj = ln == j ? cj[j] - sd : 0.0;
-    ajj = readlane_d(ajj, j);
-    if (uni(ajj <= 0.0)) {   // potf2: a NaN goes on to the square root
+    ajj = bcast<H>(ajj, j);
+    if (uniH<H>(ajj <= 0.0)) {   // potf2: a NaN goes on to the square root
       if (ln == j) cj[j] = ajj;
       lanes_sync();
       return j + 1;
@@ -239,10 +256,11 @@ __device__ __forceinline__ int ob_potrf_u(int n, double* a, int lda, Lanes L) {
 
 // dtrtrs('U', 'T', 'N') with one right-hand side (trsv_TUN); 0 or the index
 // + 1 of a zero diagonal (checked first, as dtrtrs does)
+template <bool H = false>
 NEMO_LB int ob_trsv_tun(int n, const double* u, int ldu, double* b) {
 #pragma clang fp contract(off)
   for (int i = 0; i < n; ++i)
-    if (uni(u[i + (long)i * ldu] == 0.0)) return i + 1;
+    if (uniH<H>(u[i + (long)i * ldu] == 0.0)) return i + 1;
   for (int i = 0; i < n; ++i) {
     const double* ci = u + (long)i * ldu;
     if (i > 0) b[i] = b[i] - ob_ddot(i, ci, b);
@@ -252,10 +270,11 @@ NEMO_LB int ob_trsv_tun(int n, const double* u, int ldu, double* b) {
 }
 
 // dtrtrs('U', 'N', 'N') with one right-hand side (trsv_NUN)
+template <bool H = false>
 NEMO_LB int ob_trsv_nun(int n, const double* u, int ldu, double* b) {
 #pragma clang fp contract(off)
   for (int i = 0; i < n; ++i)
-    if (uni(u[i + (long)i * ldu] == 0.0)) return i + 1;
+    if (uniH<H>(u[i + (long)i * ldu] == 0.0)) return i + 1;
   for (int j = n - 1; j >= 0; --j) {
     const double* cj = u + (long)j * ldu;
     b[j] = b[j] / cj[j];
@@ -268,10 +287,11 @@ NEMO_LB int ob_trsv_nun(int n, const double* u, int ldu, double* b) {
 // dtrtrs('U', 'T', 'N') with nrhs >= 2 (trsm_LTUN: the inverted diagonal,
 // row blocks of 16 then 8, 4, 2, 1), n <= 16, B n x nrhs (ldb); one
 // right-hand side per lane
+template <bool H = false>
 NEMO_LB int ob_trsm_lt(int n, int nrhs, const double* u, int ldu, double* b, int ldb, Lanes L) {
 #pragma clang fp contract(off)
   for (int i = 0; i < n; ++i)
-    if (uni(u[i + (long)i * ldu] == 0.0)) return i + 1;
+    if (uniH<H>(u[i + (long)i * ldu] == 0.0)) return i + 1;
   for (int j = L.id; j < nrhs; j += L.n) {
     double* x = b + (long)j * ldb;
     int r0 = 0;
@@ -330,6 +350,7 @@ NEMO_LB void matupd(Mem& mem, Ring& rg, double s, double y, double ssd, double s
 
 // formt: T = theta SS + L D^-1 L' and its Cholesky factor; returns info.
 // T's upper triangle: one entry per lane.
+template <bool H = false>
 NEMO_LB int formt(Mem& mem, const Ring& rg, double theta, Lanes L) {
 #pragma clang fp contract(off)
   const int col = rg.col;
@@ -348,13 +369,14 @@ NEMO_LB int formt(Mem& mem, const Ring& rg, double theta, Lanes L) {
     }
   }
   lanes_sync();
-  return ob_potrf_u(col, wt, kLdT, L);
+  return ob_potrf_u<H>(col, wt, kLdT, L);
 }
 
 // formk for n = nsub = 1, the variable free and staying free: WN (upper,
 // 2col x 2col, ld 2m) and its two Cholesky factorisations; info 0, -1, -2.
 // WN's entries, the solve's right-hand sides and the (2,2) block's updates:
 // one per lane.
+template <bool H = false>
 NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
 #pragma clang fp contract(off)
   const int col = rg.col, c2 = 2 * col;
@@ -376,10 +398,10 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
     at(r, c) = v;
   }
   lanes_sync();
-  if (ob_potrf_u(col, wn, kLdN, L) != 0) return -1;
+  if (ob_potrf_u<H>(col, wn, kLdN, L) != 0) return -1;
   // L^-1 (-L_a' + R_z') in the (1,2) block: one dtrtrs call with nrhs = col
   double* b12 = wn + (long)col * kLdN;
-  const int info = col == 1 ? ob_trsv_tun(1, wn, kLdN, b12) : ob_trsm_lt(col, col, wn, kLdN, b12, kLdN, L);
+  const int info = col == 1 ? ob_trsv_tun<H>(1, wn, kLdN, b12) : ob_trsm_lt<H>(col, col, wn, kLdN, b12, kLdN, L);
   if (info != 0) return -1;
   for (int t = L.id; t < kM * col; t += L.n) {
     const int a = t % kM, b = t / kM;
@@ -388,13 +410,14 @@ NEMO_LB int formk(Mem& mem, const Ring& rg, double theta, Lanes L) {
     at(is, js) = at(is, js) + ob_ddot(col, wn + (long)is * kLdN, wn + (long)js * kLdN);
   }
   lanes_sync();
-  if (ob_potrf_u(col, wn + col + (long)col * kLdN, kLdN, L) != 0) return -2;
+  if (ob_potrf_u<H>(col, wn + col + (long)col * kLdN, kLdN, L) != 0) return -2;
   return 0;
 }
 
 // subsm from z = x with r = -g (cmprlb, unconstrained): the Newton step;
 // false when a triangular solve is singular (the caller restarts)
 #if !defined(__HIP_DEVICE_COMPILE__)
+template <bool H = false>
 NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z, Lanes) {
 #pragma clang fp contract(off)
   const int col = rg.col, c2 = 2 * col;
@@ -404,9 +427,9 @@ NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, d
     wv[col + i] = theta * sum0(mem.ws(i), r);
   }
   const double* wn = mem.wn();
-  if (ob_trsv_tun(c2, wn, kLdN, wv) != 0) return false;
+  if (ob_trsv_tun<H>(c2, wn, kLdN, wv) != 0) return false;
   for (int i = 0; i < col; ++i) wv[i] = -wv[i];
-  if (ob_trsv_nun(c2, wn, kLdN, wv) != 0) return false;
+  if (ob_trsv_nun<H>(c2, wn, kLdN, wv) != 0) return false;
   double d = r;
   for (int jy = 0; jy < col; ++jy) d = d + mem.wy(jy) * wv[jy] / theta + mem.ws(jy) * wv[col + jy];
   d = d * (1.0 / theta);
@@ -420,6 +443,7 @@ NEMO_LB bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, d
 // of ddot's order; rows >= 16 take ddot's 16-term block sum at step 16), and
 // trsv_NUN's axpy updates applied by each lane to its own entry -- so a step
 // costs one operation, not a dot product.
+template <bool H = false>
 __device__ __forceinline__ bool subsm(Mem& mem, const Ring& rg, double theta, double r, double x, double& z,
                                       Lanes L) {
 #pragma clang fp contract(off)
@@ -427,7 +451,7 @@ __device__ __forceinline__ bool subsm(Mem& mem, const Ring& rg, double theta, do
   const int ln = L.id;
   const double* wn = mem.wn();
   for (int i = 0; i < c2; ++i)   // dtrtrs checks the diagonal first (both solves: the same diagonal)
-    if (uni(wn[i + (long)i * kLdN] == 0.0)) return false;
+    if (uniH<H>(wn[i + (long)i * kLdN] == 0.0)) return false;
   double b = 0.0;
   if (ln < col) b = sum0(mem.wy(ln), r);
   else if (ln < c2) b = theta * sum0(mem.ws(ln - col), r);
@@ -438,10 +462,10 @@ __device__ __forceinline__ bool subsm(Mem& mem, const Ring& rg, double theta, do
     if (k == 16 && ln >= 16 && ln < c2) {   // ddot_k, n >= 16: 4 x 4 lanes over the first 16
       double t[4];
       for (int l = 0; l < 4; ++l) {
-        const double a0 = fma_(ucol[l], readlane_d(b, l), 0.0);
-        const double a1 = fma_(ucol[4 + l], readlane_d(b, 4 + l), 0.0);
-        const double a2 = fma_(ucol[8 + l], readlane_d(b, 8 + l), 0.0);
-        const double a3 = fma_(ucol[12 + l], readlane_d(b, 12 + l), 0.0);
+        const double a0 = fma_(ucol[l], bcast<H>(b, l), 0.0);
+        const double a1 = fma_(ucol[4 + l], bcast<H>(b, 4 + l), 0.0);
+        const double a2 = fma_(ucol[8 + l], bcast<H>(b, 8 + l), 0.0);
+        const double a3 = fma_(ucol[12 + l], bcast<H>(b, 12 + l), 0.0);
         t[l] = ((a0 + a1) + a2) + a3;
       }
       dot = (t[0] + t[2]) + (t[1] + t[3]);
@@ -450,19 +474,19 @@ __device__ __forceinline__ bool subsm(Mem& mem, const Ring& rg, double theta, do
       if (k > 0) b = b - dot;
       b = b / ucol[k];
     }
-    const double bk = readlane_d(b, k);
+    const double bk = bcast<H>(b, k);
     if (ln > k && ln < c2 && (ln < 16 || k >= 16)) dot = fma_(bk, ucol[k], dot);
   }
   if (ln < col) b = -b;
   // trsv_NUN: b_j /= u_jj, then b_k -= b_j u_kj for k < j
   for (int j = c2 - 1; j >= 0; --j) {
     if (ln == j) b = b / wn[j + (long)j * kLdN];
-    const double nb = -readlane_d(b, j);
+    const double nb = -bcast<H>(b, j);
     if (ln < j) b = fma_(nb, wn[ln + (long)j * kLdN], b);
   }
   double d = r;
   for (int jy = 0; jy < col; ++jy)
-    d = d + mem.wy(jy) * readlane_d(b, jy) / theta + mem.ws(jy) * readlane_d(b, col + jy);
+    d = d + mem.wy(jy) * bcast<H>(b, jy) / theta + mem.ws(jy) * bcast<H>(b, col + jy);
   d = d * (1.0 / theta);
   z = x + d;   // the projection step of L-BFGS-B 3.0 (no bounds: alpha = 1, same bits)
   return true;
@@ -517,6 +541,7 @@ NEMO_LB void lbx_feed(LbxState& S, double f0, double f1) {
 
 // true: evaluate at (S.x_eval, S.x1) and lbx_feed; false: done, the result
 // in S.x, S.f, S.nit, S.nfev, S.status
+template <bool H = false>
 NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
 #pragma clang fp contract(off)
   using namespace lb;
@@ -524,7 +549,7 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
   const double tol = (0.01 / kEpsMch) * kEpsMch;
   const double pgtol = 0.01;
   const int maxls = 20, maxiter = 15000, maxfun = 15000;
-  const lbx::Lanes L = lbx::lanes();
+  const lbx::Lanes L = lbx::lanes<H>();
   auto restart = [&]() {
     S.rg = lbx::Ring{};
     S.theta = 1.0;
@@ -537,39 +562,39 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
   for (;;) {
     // ---- the single evaluation site (the ScalarFunction memoises the last
     // point: a repeated x costs no evaluation)
-    if (uni(!(S.have_last && S.x_eval == S.x_last))) {
+    if (uniH<H>(!(S.have_last && S.x_eval == S.x_last))) {
       const double xe = S.x_eval;
       double h = 1e-8;
-      if (uni((xe + h) - xe == 0.0)) h = kSqrtEps * (xe >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(xe));
+      if (uniH<H>((xe + h) - xe == 0.0)) h = kSqrtEps * (xe >= 0.0 ? 1.0 : -1.0) * dmax(1.0, fabs(xe));
       S.x1 = xe + h;
       return true;
     }
     double x = S.x_eval, f = S.f_last, g = S.g_last;
-    if (uni(!S.in_ls)) {
-      if (uni(fabs(g) <= pgtol)) { S.nit = 0; return done(x, f, 0); }
+    if (uniH<H>(!S.in_ls)) {
+      if (uniH<H>(fabs(g) <= pgtol)) { S.nit = 0; return done(x, f, 0); }
     } else {
       double stp = S.stp;
       int task;
-      NEMO_LBX_T(0, task = S.ls.step(stp, f, lbx::prod0(g, S.d)));
+      NEMO_LBX_T(0, task = S.ls.template step<H>(stp, f, lbx::prod0(g, S.d)));
       S.stp = stp;
-      if (uni(task == 0)) {
+      if (uniH<H>(task == 0)) {
         ++S.ifun;
-        if (uni(S.ifun - 1 < maxls)) {
+        if (uniH<H>(S.ifun - 1 < maxls)) {
           S.x_eval = (stp == 1.0) ? S.z : stp * S.d + S.xk;
           continue;
         }
         task = -1;
       }
-      if (uni(task < 0)) {  // line search failed: previous iterate, restart or give up
+      if (uniH<H>(task < 0)) {  // line search failed: previous iterate, restart or give up
         x = S.xk; f = S.fold; g = S.gold;
-        if (uni(S.rg.col == 0)) return done(x, f, 2);
+        if (uniH<H>(S.rg.col == 0)) return done(x, f, 2);
         restart();
       } else {
         ++S.nit;
-        if (uni(fabs(g) <= pgtol)) return done(x, f, 0);
+        if (uniH<H>(fabs(g) <= pgtol)) return done(x, f, 0);
         const double fold = S.fold;
-        if (uni((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))) return done(x, f, 1);
-        if (uni(S.nit >= maxiter || S.nfev > maxfun)) return done(x, f, 3);
+        if (uniH<H>((fold - f) <= tol * dmax(dmax(fabs(fold), fabs(f)), 1.0))) return done(x, f, 1);
+        if (uniH<H>(S.nit >= maxiter || S.nfev > maxfun)) return done(x, f, 3);
         double d = S.d;
         const double gdold = S.gdold;
         const double gd = lbx::prod0(g, d);
@@ -579,7 +604,7 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
         if (stp == 1.0) { dr = gd - gdold; ddum = -gdold; }
         else { dr = (gd - gdold) * stp; d = d * stp; ddum = -gdold * stp; }
         S.d = d;
-        if (uni(dr <= kEpsMch * ddum)) {
+        if (uniH<H>(dr <= kEpsMch * ddum)) {
           S.updatd = false;
         } else {
           S.updatd = true;
@@ -588,8 +613,8 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
           lbx::matupd(mem, rg, d, r, (stp == 1.0) ? S.dtd : stp * stp * S.dtd, dr);
           S.rg = rg;
           int ft;
-          NEMO_LBX_T(1, ft = lbx::formt(mem, rg, S.theta, L));
-          if (uni(ft != 0)) restart();
+          NEMO_LBX_T(1, ft = lbx::formt<H>(mem, rg, S.theta, L));
+          if (uniH<H>(ft != 0)) restart();
         }
       }
     }
@@ -597,7 +622,7 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
     for (;;) {
       double z;
       const double theta = S.theta;
-      if (uni(S.rg.col == 0)) {
+      if (uniH<H>(S.rg.col == 0)) {
         const double neggi = -g;
         const double f1 = 0.0 - neggi * neggi;
         const double f2 = -theta * f1;
@@ -607,15 +632,15 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
       } else {
         const lbx::Ring rg = S.rg;
         int fk = 0;
-        if (uni(S.updatd)) NEMO_LBX_T(2, fk = lbx::formk(mem, rg, theta, L));
-        if (uni(fk != 0)) {
+        if (uniH<H>(S.updatd)) NEMO_LBX_T(2, fk = lbx::formk<H>(mem, rg, theta, L));
+        if (uniH<H>(fk != 0)) {
           restart();
           continue;
         }
         double zz = x;
         bool ok;
-        NEMO_LBX_T(3, ok = lbx::subsm(mem, rg, theta, -g, x, zz, L));
-        if (uni(!ok)) {
+        NEMO_LBX_T(3, ok = lbx::subsm<H>(mem, rg, theta, -g, x, zz, L));
+        if (uniH<H>(!ok)) {
           restart();
           continue;
         }
@@ -631,16 +656,16 @@ NEMO_LB bool lbx_run(LbxState& S, lbx::Mem mem) {
       S.xk = x; S.fold = f; S.gold = g;
       const double gdold = lbx::prod0(g, d);
       S.gdold = gdold;
-      if (uni(gdold < 0.0)) {
+      if (uniH<H>(gdold < 0.0)) {
         S.ls.stpmax = kStpMax;
-        S.ls.start(stp, f, gdold);
+        S.ls.template start<H>(stp, f, gdold);
         S.ifun = 1;
         S.in_ls = true;
         S.x_eval = (stp == 1.0) ? z : stp * d + x;
         break;
       }
       // lnsrlb: the directional derivative is not negative (info = -4)
-      if (uni(S.rg.col == 0)) return done(x, f, 2);
+      if (uniH<H>(S.rg.col == 0)) return done(x, f, 2);
       restart();
     }
   }

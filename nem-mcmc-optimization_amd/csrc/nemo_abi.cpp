@@ -1451,9 +1451,9 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "exact_form") == 0) {
-    if (value < 0 || value > 4)
-      return fail(NEMO_ERR_ARG, "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair, 4 cached throughput)",
-                  value);
+    if (value < 0 || value > 5)
+      return fail(NEMO_ERR_ARG,
+                  "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair, 4 cached throughput, 5 dual)", value);
     ctx->c.exact_form = value;
     return NEMO_OK;
   }

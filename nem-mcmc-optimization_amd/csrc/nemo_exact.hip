@@ -22,6 +22,8 @@
 #include "nemo_internal.h"
 #include "refmath.h"
 
+#include <type_traits>
+
 // no multiply-add is fused in this file but the explicit fma() calls (HIP's
 // default contraction would fuse them; the functions repeat the pragma)
 #pragma clang fp contract(off)
@@ -487,7 +489,7 @@ struct ExactObjective {
         a1 = a1 + t1;
       }
     };
-    if (kLat) {
+    if (kLat || kCache) {   // (a cached c needs constant indices: a loop index would put it in scratch)
       double c[kChain];
 #pragma unroll
       for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
@@ -883,6 +885,235 @@ __global__ __launch_bounds__(2 * kWave) __attribute__((amdgpu_waves_per_eu(4, 4)
   }
 }
 
+// The dual form (option exact_form 5): two optima per wave.  Half h of the
+// wave (lanes 32 h .. 32 h + 31) runs optimum h's control -- lbfgsb_exact.h
+// with H = true: the same operations spread over 32 lanes instead of 64, its
+// branches divergent by half -- and every lane holds BOTH optima's c values
+// at its plan positions (the latency form's register cache, twice), so one
+// pass of the objective makes both optima's forward differences.  Two optima
+// share each control instruction the halves take together, and each pass of
+// the objective carries twice the independent logs.  Each optimum's rounded
+// operations are those of the one-wave forms, so the bits are the same.
+template <int NS>
+struct DualObjective {
+  static constexpr int kChain = 16;
+  static constexpr int kRows = kChain + 1;
+  double cc[2][NS][kRows];   // optimum o's c values at this lane's plan positions
+  const int32_t* pl;         // host::PairwisePlan rows in LDS (ExactObjective)
+  int nh, maxrem, lane;
+  LdsTabs tb;
+
+  __device__ __forceinline__ int cnt(int u) const { return pl[(NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int rem(int u) const { return pl[(2 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int nrem(int u) const { return pl[(3 * NS + u) * kWave + lane]; }
+  __device__ __forceinline__ int partner(int h) const { return pl[(4 * NS + h) * kWave + lane]; }
+
+  // optimum o's c = a / ((1 - s a) + s (lv - 1)) from its parent's
+  // plan-ordered a rows (ExactObjective::rc_c, fill_cache)
+  template <int o>
+  __device__ __forceinline__ void fill(const double* __restrict__ cp, const uint32_t* rbits, double rs, double rslo,
+                                       double rshi, bool pad_guard) {
+#pragma clang fp contract(off)
+    auto cv = [&](int u, int m, bool real) {
+      const double a = cp[(u * kRows + m) * kWave + lane];
+      const double sl = ((rbits[u] >> m) & 1u) ? rshi : rslo;
+      const double bd = (1.0 - rs * a) + sl;
+      const double c = a / bd;
+      return pad_guard ? (real ? c : 0.0) : c;
+    };
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int cu = cnt(u);
+#pragma unroll
+      for (int m = 0; m < kChain; ++m) cc[o][u][m] = cv(u, m, m < cu);
+      cc[o][u][kChain] = cv(u, kChain, rem(u) >= 0);
+    }
+  }
+
+  // slot u's chain sums of the four points (optimum o, point p: a[2 o + p]),
+  // each as ExactObjective::slot_sums makes it
+  __device__ __forceinline__ void slot_sums(int u, const double (&ex)[4], double (&a)[4]) const {
+#pragma clang fp contract(off)
+    // fully unrolled: the cache is registers only while every index is a
+    // constant (a loop index would put it in scratch); one element's four
+    // logs at a time in the schedule
+#pragma unroll
+    for (int m = 0; m < kChain; ++m) {
+      double t[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = refmath::svml_log(cc[q >> 1][u][m] * ex[q] + 1.0, tb);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = m == 0 ? t[q] : a[q] + t[q];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int d = 1; d <= 4; d <<= 1)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = a[q] + __shfl_xor(a[q], d);
+    if (lb::uni(maxrem > 0)) {
+      const int ru = rem(u), nr = nrem(u);
+      double tr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tr[q] = ru >= 0 ? refmath::svml_log(cc[q >> 1][u][kChain] * ex[q] + 1.0, tb) : 0.0;
+      for (int r = 0; r < 7; ++r) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double y = __shfl(tr[q], (lane & ~7) + r);
+          a[q] = r < nr ? a[q] + y : a[q];
+        }
+      }
+    }
+  }
+
+  // ExactObjective::tree for the four sums
+  __device__ __forceinline__ void tree(const double (&res)[NS][4], double (&s)[4]) const {
+#pragma clang fp contract(off)
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < NS; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double x = __shfl(res[u][q], 8 * (lane & 7));
+        v[q] = (lane >> 3) == u ? x : v[q];
+      }
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      if (!lb::uni(h < nh)) break;
+      const int p = partner(h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double y = __shfl(v[q], p < 0 ? lane : p);
+        v[q] = p >= 0 ? v[q] + y : v[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] = __shfl(v[q], 0);
+  }
+
+  // f at x[q] (optimum q >> 1, point q & 1), local_ll_sum_penalized (:18-23)
+  __device__ __forceinline__ void operator()(const double (&x)[4], double anc0, double anc1, double (&f)[4]) const {
+#pragma clang fp contract(off)
+    double e[4], res[NS][4], p[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = refmath::expit(x[q], tb);
+#pragma unroll
+    for (int u = 0; u < NS; ++u) slot_sums(u, e, res[u]);
+    tree(res, p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f[q] = (-p[q] + fabs(e[q] - (q < 2 ? anc0 : anc1))) + e[q] * (1.0 - e[q]);
+  }
+};
+
+template <int NS>
+__global__ __launch_bounds__(kExactWaves * kWave) __attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_dual_kernel(
+    int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
+    const double* __restrict__ anc, const double* __restrict__ xlo, const double* __restrict__ xhi,
+    const int32_t* __restrict__ plan, int nh, int maxrem, double sig0, double sig1, double* __restrict__ wnew,
+    double* __restrict__ wdag, int32_t* __restrict__ info, CArgs ca, int lo_blocks, SeqSumArgs fin) {
+#pragma clang fp contract(off)
+  __shared__ TabsLds tabs;
+  __shared__ double mem[kExactWaves][2][lbx::kMemDoubles];
+  __shared__ double lst_raw[kExactWaves][2][kStateDoubles];
+  __shared__ int32_t pl[(4 * NS + 8) * kWave];
+  const int wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  if ((int)blockIdx.x >= lo_blocks) {   // one wave per chain: eval #1's ll
+    const int bb = __builtin_amdgcn_readfirstlane(((int)blockIdx.x - lo_blocks) * kExactWaves + wv);
+    if (bb < fin.batch) {
+      const double v = wave_seq_sum(fin.cs + (size_t)bb * fin.E, fin.E, lane, &mem[wv][0][0]);
+      if (lane == 0) fin.ll[bb] = v;
+    }
+    return;
+  }
+  tabs.fill(threadIdx.x, blockDim.x);
+  plan_to_lds<NS>(plan, nh, pl);
+  __syncthreads();
+  const int hf = lane >> 5;
+  const int total = nchains * npairs;
+  constexpr size_t kPlanD = (size_t)NS * DualObjective<NS>::kRows * kWave;
+  DualObjective<NS> obj;
+  obj.tb = tabs.view();
+  obj.pl = pl;
+  obj.lane = lane;
+  obj.nh = nh;
+  obj.maxrem = maxrem;
+  LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv][hf]);   // this half's optimum's state
+  const lbx::Mem mm{mem[wv][hf]};
+  // per slot (uniform): the optimum's (chain, child, parent) index and anc
+  size_t idx0 = 0, idx1 = 0;
+  double anc0 = 0.0, anc1 = 0.0;
+  // take the next optimum into slot o: its c values (every lane) and its
+  // control's start (half o); false when the queue is drained
+  auto take = [&](auto oc) -> bool {
+    constexpr int o = decltype(oc)::value;
+    const int item = next_item(ca.queue, lane);
+    if (item >= total) return false;
+    const int gw = ca.order ? __builtin_amdgcn_readfirstlane(ca.order[item]) : item;
+    const int b = gw / npairs;
+    const int n = gw - b * npairs;
+    const int pk = pairs[(size_t)b * S * S + n];
+    const int i = pk >> 16;
+    const int k = pk & 0xffff;
+    const size_t idx = ((size_t)b * S + i) * S + k;
+    const double s = w01[idx];
+    uint32_t rb[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) rb[u] = ca.xbits[((size_t)k * NS + u) * kWave + lane];
+    const double rslo = s * (xlo[k] - 1.0), rshi = s * (xhi[k] - 1.0);
+    obj.template fill<o>(ca.xa + ((size_t)b * S + k) * kPlanD, rb, s, rslo, rshi,
+                         __builtin_amdgcn_readfirstlane((int)(1.0 + rslo == 0.0)) != 0);
+    if (o == 0) idx0 = idx, anc0 = anc[idx];
+    else idx1 = idx, anc1 = anc[idx];
+    if (hf == o) lbx_init(st, s);
+    return true;
+  };
+  // One call site of the control (every inlined copy costs registers next to
+  // the two caches): passes over the halves that need their next point --
+  // after an evaluation, or a fresh optimum its first -- until both have one
+  // or are drained; an optimum that ends hands its slot to the next one,
+  // which then needs a pass of its own
+  bool act0 = false, act1 = false;
+  bool need0 = false, need1 = false;
+  uint64_t ended = ~0ull;   // both slots take their first optimum
+  for (;;) {
+    for (;;) {
+      if (ended & 1ull) need0 = act0 = take(std::integral_constant<int, 0>{});
+      if (ended >> 32) need1 = act1 = take(std::integral_constant<int, 1>{});
+      const bool run = hf ? need1 : need0;
+      if (__ballot(run) == 0ull) break;
+      const bool more = run ? lbx_run<true>(st, mm) : false;
+      const bool done = run && !more;
+      if (done && (lane & 31) == 0) {   // optimum hf ended: its outputs (as local_opt_exact_kernel)
+        const size_t idx = hf ? idx1 : idx0;
+        const double wx = refmath::expit(st.x, obj.tb);
+        wnew[idx] = wx;
+        wdag[idx] = (wx > 0.5) ? sig1 : sig0;
+        if (info) {
+          const int nit = st.nit < 4095 ? st.nit : 4095;
+          const int nfev = st.nfev < 32767 ? st.nfev : 32767;
+          info[idx] = (int32_t)(st.status | (nit << 4) | (nfev << 16));
+        }
+        if (ca.cost) ca.cost[idx] = st.nfev;
+      }
+      ended = __ballot(done);
+      need0 = need1 = false;
+    }
+    if (!act0 && !act1) break;
+    // both points of both optima (a drained slot's stale points are evaluated
+    // and ignored)
+    lbx::lanes_sync();
+    const LbxState& s0 = *reinterpret_cast<const LbxState*>(lst_raw[wv][0]);
+    const LbxState& s1 = *reinterpret_cast<const LbxState*>(lst_raw[wv][1]);
+    const double x[4] = {act0 ? s0.x_eval : 0.0, act0 ? s0.x1 : 0.0, act1 ? s1.x_eval : 0.0, act1 ? s1.x1 : 0.0};
+    double f[4];
+    obj(x, anc0, anc1, f);
+    if (hf ? act1 : act0) lbx_feed(st, hf ? f[2] : f[0], hf ? f[3] : f[1]);
+    need0 = act0;
+    need1 = act1;
+    ended = 0ull;
+  }
+}
+
 // the same optimiser on caller-supplied c vectors [n][E] (nemo_local_opt:
 // calculate_local_optimum of one pair, and the scipy records of the tests);
 // out [n][3] = x*, f*, packed info
@@ -1025,6 +1256,7 @@ __global__ __launch_bounds__(kSchedThreads) void exact_sched_place_kernel(int S,
 
 }  // namespace
 
+#ifndef NEMO_EXACT_KERNELS_ONLY   // (tools/ubench: the kernels alone, for their register reports)
 hipError_t launch_local_opt_exact_generic(Ctx& c, int n, const double* d_c, const double* d_anc, const double* d_x0,
                                           double* d_out, hipStream_t st) {
   const dim3 grid((n + kExactWaves - 1) / kExactWaves);
@@ -1131,7 +1363,13 @@ int lo_resident(int form) {
 }
 
 template <int NS>
-int lo_resident_ns(int form, bool rc) { return rc ? lo_resident<NS, true>(form) : lo_resident<NS, false>(form); }
+int lo_resident_ns(int form, bool rc) {
+  if (form == 5) {
+    if constexpr (NS <= 2) return resident_blocks<local_opt_exact_dual_kernel<NS>>(kExactWaves * kWave);
+    return 0;
+  }
+  return rc ? lo_resident<NS, true>(form) : lo_resident<NS, false>(form);
+}
 
 template <int NS, bool kRc>
 void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
@@ -1155,6 +1393,13 @@ void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
 
 template <int NS>
 void launch_lo_ns(const LoArgs& a, int form, bool rc, dim3 grid, hipStream_t st) {
+  if (form == 5) {
+    if constexpr (NS <= 2)
+      local_opt_exact_dual_kernel<NS><<<grid, kExactWaves * kWave, 0, st>>>(
+          a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.xlo, a.xhi, a.plan, a.nh, a.maxrem, a.sig0, a.sig1,
+          a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+    return;
+  }
   if (rc) launch_lo<NS, true>(a, form, grid, st);
   else launch_lo<NS, false>(a, form, grid, st);
 }
@@ -1180,9 +1425,13 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves && c.pw_ns <= 3)))
     form = 3;
   if (c.pw_ns < 2 && form == 3) form = 2;
-  int lo_blocks = form == 3 ? nw : (nw + kExactWaves - 1) / kExactWaves;
   // the persistent form: at most the resident blocks, the work counter zeroed
   const bool persist = c.exact_persist && c.d_xqueue;
+  // the dual form (two optima per wave) needs the register cache's recompute
+  // rows, the work queue and at most two slots; else the latency form
+  if (form == 5 && !(rc && persist && c.pw_ns <= 2)) form = 1;
+  const int per_block = form == 3 ? 1 : form == 5 ? 2 * kExactWaves : kExactWaves;   // optima a block holds at once
+  int lo_blocks = (nw + per_block - 1) / per_block;
   if (persist) {
     int res = 0;
     switch (c.pw_ns) {
@@ -1213,7 +1462,6 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   // and make at most 16 rounds of them: past that the last optimum's share of
   // the launch is small and the chains' interleaving costs more (C3, 128
   // chains: 11.99 against 11.84 ms per step, tools/step_probe.py)
-  const int per_block = form == 3 ? 1 : kExactWaves;   // optima a block holds at once
   if (persist && c.exact_sched && c.d_xcost && c.d_xorder && c.cap_xorder >= (size_t)nw &&
       nw > lo_blocks * per_block && nw <= 16 * lo_blocks * per_block) {
     exact_sched_hist_kernel<<<nchains, kSchedThreads, 0, st>>>(c.S, npairs, d_pairs, c.d_xcost, c.d_xhist);
@@ -1226,6 +1474,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
     a.ca.order = c.d_xorder;
   }
   const dim3 grid(lo_blocks + fin_blocks);
+  if (form == 5) a.ca.trace = nullptr;   // (the dual form keeps no timeline)
   c.xtrace_n = a.ca.trace ? nw : 0;
   switch (c.pw_ns) {
     case 1: launch_lo_ns<1>(a, form, rc, grid, st); break;
@@ -1240,5 +1489,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   }
   return hipGetLastError();
 }
+
+#endif  // NEMO_EXACT_KERNELS_ONLY
 
 }  // namespace nemo

@@ -8,7 +8,7 @@ documented ``opt_weights`` pass-through, and writes small
 reference's outputs); no reference source is stored.
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py [--only-replica | --only-methods | --only-networks | --only-evals | --only-traj-c3 N | --only-traj-nem
-                                                          | --only-c3-extra]
+                                                          | --only-c3-extra | --only-capped-step]
 
 Versions at capture: see ``meta.json`` written alongside.
 """
@@ -230,6 +230,66 @@ def capture_traj(ref_mcmc, m, order, gamma, swap_prob, n_iter, name, record_loca
         print(f"localopt_{name}: {len(local)} records")
 
 
+def capture_capped_step(ref_nem, ref_mcmc, ref_utils, gen, s=40, e=333, cap=6, n_cases=3, seed=0):
+    """The capped fused step (the build-defined C5 shape):
+    one get_optimal_weights(init=True) (nem_order_mcmc.py:172-208) per case on
+    a reference sampler whose parents_list is cut to the last <= cap
+    predecessors, as ``ref_eval`` cuts it for eval_C5cap -- the cell ratios,
+    expit_parent_weights (ancestor_x), the local optima (:186-189) and the
+    dag's score all read that list.  Recorded per case: the inputs (perm, raw
+    W), the step's ll, dag_ll, ancestor_x, the new weights and, per local
+    optimum in the reference's loop order, (i, k, x0, anc, x*, nit, nfev, f*)."""
+    from scipy.optimize import minimize
+    from scipy.special import expit
+    net = gen.synthetic_network(s, e, seed)
+    m = ref_nem_without_diagnostics(ref_nem, ref_utils, net.adj.copy(), net.end_nodes, net.errors, s, e)
+    tables = m.get_score_tables(m.observed_knockdown_mat)
+    rng = np.random.default_rng(4242)
+    out = dict(S=s, E=e, seed=seed, cap=cap, A=m.A, B=m.B,
+               D_packed=np.packbits(m.observed_knockdown_mat.astype(np.uint8), axis=None))
+    for case in range(n_cases):
+        perm = rng.permutation(s)
+        w_raw = rng.uniform(-3, 3, (s, s))
+        mc = ref_mcmc.NEMOrderMCMC.__new__(ref_mcmc.NEMOrderMCMC)
+        mc.num_s, mc.num_e, mc.U = s, e, m.U.copy()
+        mc.score_tables = tables
+        mc.I = np.identity(s)
+        mc.parent_weights = np.zeros((s, s))
+        mc.get_permissible_parents(perm, init=True, init_value=1.0)
+        capped = np.empty(s, dtype=object)
+        for i, pl in enumerate(mc.parents_list):
+            capped[i] = pl[max(0, len(pl) - cap):]
+        mc.parents_list = capped
+        mc.parent_weights = w_raw.copy()
+        recs = []
+        orig = mc.calculate_local_optimum
+
+        def local_opt(i, k, mc=mc, orig=orig, recs=recs):
+            lv = np.exp(mc.score_tables[i][k])
+            a = (lv - 1.0) * mc.order_weights[k]
+            sg = expit(mc.parent_weights[i][k])
+            c = a / (1.0 - sg * a + sg * (lv - 1.0))
+            res = minimize(ref_mcmc.local_ll_sum_penalized, x0=sg, bounds=[(-float("inf"), float("inf"))],
+                           args=(c, mc.ancestor_x[i][k]), method="L-BFGS-B", tol=0.01)
+            got = orig(i, k)
+            assert got[0] == expit(res.x)[0]
+            recs.append((i, k, sg, mc.ancestor_x[i][k], res.x[0], res.nit, res.nfev, res.fun))
+            return got
+        mc.calculate_local_optimum = local_opt
+        dag_ll = quiet(mc.get_optimal_weights, init=True)
+        out[f"c{case}_perm"] = perm
+        out[f"c{case}_W"] = w_raw
+        out[f"c{case}_ll"] = mc.ll
+        out[f"c{case}_dag_ll"] = dag_ll
+        out[f"c{case}_anc"] = mc.ancestor_x
+        out[f"c{case}_W_new"] = mc.parent_weights
+        out[f"c{case}_local"] = np.array([r[:2] for r in recs], dtype=np.int64)
+        out[f"c{case}_local_f"] = np.array([r[2:5] + (r[7],) for r in recs], dtype=np.float64)
+        out[f"c{case}_local_n"] = np.array([r[5:7] for r in recs], dtype=np.int64)
+        print(f"capped step case {case}: ll={mc.ll} dag_ll={dag_ll} optima={len(recs)}")
+    np.savez_compressed(os.path.join(HERE, f"step_C5cap_{s}x{e}.npz"), n_cases=n_cases, **out)
+
+
 def capture_replica_exchange(ref_nem, ref_mcmc, ref_utils, n_exchange=3, n_iter=4, seed=2024, model=None,
                              name="net2"):
     """replica_exchange_method (nem_order_mcmc.py:344-363) on net2 (or on the
@@ -408,6 +468,9 @@ def main():
                                  model=(mc3, order3), name="C3")
         random.seed(77)
         capture_traj(ref_mcmc, mc3, order3, 2.0 * 64 / 2000, 0.95, 20, "C3_nem_20", use_nem=True)
+        return
+    if "--only-capped-step" in sys.argv:
+        capture_capped_step(ref_nem, ref_mcmc, ref_utils, gen)
         return
     if "--only-evals" in sys.argv:
         capture_evals(ref_nem, ref_mcmc, ref_utils, gen, "C3", 64, 2000, 0, 0, 32, True)

@@ -251,6 +251,45 @@ def test_exact_capped_fused_step_equals_oracle_c5():
         eng.close()
 
 
+def test_exact_capped_step_equals_reference_capture():
+    """The capped step pinned to the reference itself (not only to the
+    oracle): tests/golden/step_C5cap_40x333.npz holds three
+    get_optimal_weights(init=True) steps of the reference with its
+    parents_list cut to the last 6 predecessors (the C5 shape on a 40 x 333
+    model; nem_order_mcmc.py:172-208, :186-189).  The sampler's fused step
+    from W (W~ and ancestor_x on the device) gives the same ll, dag_ll,
+    ancestor_x and new weights, and every local optimum the reference's nit
+    and nfev, to the bit."""
+    from nemo.nem_order_mcmc import NEMOrderMCMC, SIG0, SIG1
+    z = golden("step_C5cap_40x333.npz")
+    s, e, cap = int(z["S"]), int(z["E"]), int(z["cap"])
+    m = generator.synthetic_nem(s, e, int(z["seed"]))
+    d = np.unpackbits(z["D_packed"])[: s * e].reshape(s, e)
+    assert np.array_equal(m.observed_knockdown_mat, d)
+    eng = Engine.for_nem(m)
+    assert eng.get_option("exact_ok") == 1
+    try:
+        for c in range(int(z["n_cases"])):
+            perm = z[f"c{c}_perm"]
+            smp = NEMOrderMCMC(m, perm, engine=eng, cap=cap)
+            smp.parent_weights = np.array(z[f"c{c}_W"], copy=True)
+            got_dag = smp.get_optimal_weights(init=True)
+            assert smp.ll == z[f"c{c}_ll"] and got_dag == z[f"c{c}_dag_ll"], c
+            assert _bits_equal(smp.parent_weights, z[f"c{c}_W_new"]), c
+            assert _bits_equal(smp.ancestor_x, z[f"c{c}_anc"]), c
+            # the optimiser's own counts, pair by pair
+            pos = np.empty(s, dtype=np.int32)
+            pos[perm] = np.arange(s)
+            *_, info = eng.optimal_weights_w(pos[None], z[f"c{c}_W"][None], SIG0, SIG1, cap=cap,
+                                             raise_on_fail=False)
+            ik, n = z[f"c{c}_local"], z[f"c{c}_local_n"]
+            inf = info[0][ik[:, 0], ik[:, 1]]
+            assert np.array_equal((inf >> 4) & 0xfff, n[:, 0]) and np.array_equal(inf >> 16, n[:, 1]), c
+            assert ((info[0] != -1).sum()) == len(ik)
+    finally:
+        eng.close()
+
+
 def test_exact_capped_scores_equal_golden_c5():
     """The capped order scores of the C5 golden (the reference's own
     calculate_ll with parents_list cut to the last 6 predecessors,
@@ -302,8 +341,8 @@ def test_exact_score_cells_and_order_weights_together():
 
 
 def test_exact_kernel_forms_give_the_same_bits():
-    """The local-optimum kernel's latency, throughput and pair forms (option
-    exact_form 1 / 2 / 3), c stored or recomputed (exact_cform 0 / 1), in
+    """The local-optimum kernel's latency, throughput, pair, cached
+    throughput and dual forms (option exact_form 1 / 2 / 3 / 4 / 5), c stored or recomputed (exact_cform 0 / 1), in
     launch order or XCD-contiguous order (exact_xcd): the same weights, dag
     weights and lls, to the bit, for one chain and for three."""
     from nemo.nem_order_mcmc import SIG0, SIG1
@@ -316,7 +355,7 @@ def test_exact_kernel_forms_give_the_same_bits():
         anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
         outs = []
         try:
-            for form in (1, 2, 3):
+            for form in (1, 2, 3, 4, 5):
                 for cform in (0, 1):
                     for xcd in (0, 1):
                         eng.set_option("exact_form", form)

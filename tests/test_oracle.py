@@ -137,3 +137,31 @@ def test_oracle_trajectory_net2_use_nem_50(net2):
     assert np.array_equal(smp.best_order, z["best_order"])
     assert np.array_equal(smp.w, z["final_W"])
     assert np.array_equal(np.array(random.getstate()[1]), z["rng_state_after"])
+
+
+def test_oracle_capped_step_equals_reference_capture():
+    """The capped step (the C5 shape, parent lists cut to the last 6
+    predecessors): OracleSampler(cap=6)'s get_optimal_weights(init=True)
+    equals the reference's own step on the same cut lists
+    (tests/golden/make_goldens.py capture_capped_step, nem_order_mcmc.py:
+    172-208 with :186-189 over the overridden parents_list) -- ll, dag_ll,
+    ancestor_x, the new weights and every local optimum's x*, nit and nfev, to
+    the bit.  This pins the oracle's cap branch (nemo_oracle.py permissible)."""
+    z = golden("step_C5cap_40x333.npz")
+    d = _unpack_d(z)
+    a, b = float(z["A"]), float(z["B"])
+    tt = no.score_tensor(d, a, b)
+    u = no.node_lr_table(tt, d, a)
+    cap = int(z["cap"])
+    for c in range(int(z["n_cases"])):
+        ora = no.OracleSampler(u, tt, z[f"c{c}_perm"], record_local=True, cap=cap)
+        ora.w = np.array(z[f"c{c}_W"], copy=True)
+        dag_ll = ora.optimal_weights()
+        assert ora.ll1 == z[f"c{c}_ll"] and dag_ll == z[f"c{c}_dag_ll"]
+        assert np.array_equal(ora.anc, z[f"c{c}_anc"])
+        assert np.array_equal(ora.w, z[f"c{c}_W_new"])
+        ik = z[f"c{c}_local"]
+        assert [(r[0], r[1]) for r in ora.local_log] == [tuple(x) for x in ik.tolist()]
+        got_f = np.array([(r[4], r[3], r[5]) for r in ora.local_log])   # x0, anc, x*
+        assert np.array_equal(got_f, z[f"c{c}_local_f"][:, :3])
+        assert np.array_equal(np.array([(r[6], r[7]) for r in ora.local_log]), z[f"c{c}_local_n"])
