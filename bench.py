@@ -437,6 +437,51 @@ def score_roofline(config, S, E, cap, B, fk, kern_ms, launch_ev_ms, bid):
     return roof
 
 
+# The exact local optima's kernel (local_opt_exact_kernel, nemo_exact.hip): where the sampler's
+# step spends its time.  Priced on the SIMDs' VALU issue: its unit of work is one
+# f-evaluation of the reference's objective (nem_order_mcmc.py:18-23), E terms log(c e + 1)
+# summed, at LOG_VALU wave instructions per 64 terms -- svml_log as restated (refmath.h: 14 for
+# the reduction and the table row, 16 for the polynomial and the reconstruction) plus the product,
+# the + 1 and the sum's add -- each 4 SIMD cycles.  The f-evaluations of a launch
+# are the optima's nfev (the info array); the kernel's time from HIP events around its launch
+# (option timing_kernel 1).  The control of L-BFGS-B and the tree of the pairwise sum are not
+# priced: the fraction says how far the launch is from the objective's own VALU work.
+LOG_VALU = 33
+SIMD_CYCLES_PER_S = 1024 * 2.4e9
+
+
+def local_opt_roofline(eng, S, E, cap, chains, reps=5):
+    from scipy.special import expit
+
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    rng = np.random.default_rng(11 + chains)
+    pos = np.array([rng.permutation(S) for _ in range(chains)], dtype=np.int32)
+    w = rng.uniform(-3, 3, (chains, S, S))
+    w01 = expit(w)
+    anc = np.clip(rng.random((chains, S, S)) - 0.5, 0, 1)
+    eng.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap, raise_on_fail=False)
+    eng.set_option("timing_kernel", 1)
+    eng.timing(True)
+    try:
+        for _ in range(reps):
+            _, _, _, info = eng.optimal_weights(pos, w01, anc, w, SIG0, SIG1, cap=cap, raise_on_fail=False)
+        ms, n = eng.timing_read()
+    finally:
+        eng.timing(False)
+        eng.set_option("timing_kernel", 0)
+    kern_ms = ms / max(n, 1)
+    inf = info[info != -1]
+    nfev = int(((inf >> 16) & 0x7fff).sum())
+    work = nfev * E * LOG_VALU / 64.0 * 4.0          # VALU-busy SIMD cycles of the objective
+    achieved = work / (kern_ms * 1e-3) / 1e12
+    peak = SIMD_CYCLES_PER_S / 1e12
+    return {"chains": chains, "optima": int(inf.size), "f_evaluations": nfev, "kernel_avg_ms": kern_ms,
+            "launches_timed": n, "exact_form": eng.get_option("exact_form"),
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "T VALU-busy SIMD-cycles/s",
+                         "frac": achieved / peak, "traffic": None,
+                         "work": f"f-evaluations x E x {LOG_VALU} VALU / 64 lanes x 4 cycles"}}
+
+
 def c3_fp64(eng, torch, dist, B, cap, d_pos, d_w01, stream, S, E, ll_ref, steps=10, warmup_s=0.3):
     """The headline workload (same model, same resident inputs, same B) in
     fp64 arithmetic: the fp64 MFMA factored kernels (fact_kernel 2: pipelined,
@@ -667,6 +712,11 @@ def main():
         fs_fast = fused_ms(nch, 5)
         fs1_fast = fused_ms(1, 20)
         eng.set_option("exact", 1)
+        if exact_on:
+            extras["local_opt"] = {
+                "kernel": "local_opt_exact_kernel (scipy's L-BFGS-B per (chain, parent pair), the reference's bits)",
+                "c16": local_opt_roofline(eng, S, E, cap, nch),
+                "c128": local_opt_roofline(eng, S, E, cap, 128, reps=3)}
         extras["mcmc_fused_step"] = {
             "chains": nch, "ms_per_step": 1e3 * fs, "chain_steps_per_s": nch / fs,
             "arithmetic": "exact (the reference's bits)" if exact_on else "fast",

@@ -59,20 +59,35 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIPCHK(expr)                                                                    \
-  do {                                                                                  \
-    hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess)                                                               \
-      return fail(NEMO_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+// A HIP failure's message, with the process's FIRST HIP failure beside it when
+// this one differs: an asynchronous fault sticks and is then reported by every
+// later call under its own name (a capture conflict resurfaced as "invalid
+// device ordinal"), so the first failure is what names the cause
+int fail_hip(const char* what, hipError_t e) {
+  static std::mutex mu;
+  static std::string first;
+  std::string cur = std::string(what) + " failed: " + hipGetErrorString(e);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (first.empty()) first = cur;
+    else if (first != cur) cur += " (the first HIP error in this process: " + first + ")";
+  }
+  return fail(NEMO_ERR_HIP, "%s", cur.c_str());
+}
+
+#define HIPCHK(expr)                                    \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return fail_hip(#expr, e_);   \
   } while (0)
 
-// One process-wide lock around graph capture and the calls that allocate,
-// free, or use the legacy stream (staging, reserve, context create / destroy,
-// the probes): a step captured on one engine's step thread and such a call on
-// another engine in another thread must not overlap -- HIP refuses a
-// legacy-stream operation while a stream captures ("would make the legacy
-// stream depend on a capturing blocking stream"), and the error then sticks
-// to the next launch (tests/test_gpu_parity.py::test_staging_while_the_gpu_is_busy)
+// One process-wide lock around graph capture and the calls that still use the
+// legacy stream or resize a context's buffers under a running step (reserve,
+// context create / destroy, the probes): HIP refuses a legacy-stream operation
+// while a stream captures ("would make the legacy stream depend on a
+// capturing blocking stream"), and the error then sticks to the next launch.
+// Staging holds no lock: its transfers run on the context's own stream
+// (tests/test_gpu_parity.py::test_staging_while_another_engine_captures)
 std::recursive_mutex& api_mutex() {
   static std::recursive_mutex m;
   return m;
@@ -308,9 +323,9 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     HIPCHK(dalloc(&c.d_D1w, d1.size()));
     HIPCHK(dalloc(&c.d_elo, S));
     HIPCHK(dalloc(&c.d_ehi, S));
-    HIPCHK(hipMemcpy(c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
+    HIPCHK(nemo::copy_sync(c, c.d_D1w, d1.data(), d1.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(nemo::copy_sync(c, c.d_elo, elo.data(), S * 8, hipMemcpyHostToDevice));
+    HIPCHK(nemo::copy_sync(c, c.d_ehi, ehi.data(), S * 8, hipMemcpyHostToDevice));
     // int8 variants (S <= 128): per-model fixed-point scale and the D1 bytes in
     // v_mfma_i32_16x16x64_i8 B-fragment order: K half h (parents 64 h .. 64 h
     // + 63; one half for S <= 64, two for S <= 128), tile t, lane l (effect
@@ -343,7 +358,7 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
       b8.resize(2 * nb);
       for (size_t k = 0; k < nb; ++k) b8[nb + k] = (uint8_t)(b8[k] << 6);
       HIPCHK(hipMalloc((void**)&c.d_B8, b8.size()));
-      HIPCHK(hipMemcpy(c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_B8, b8.data(), b8.size(), hipMemcpyHostToDevice));
     }
     HIPCHK(nemo::stage_i8o(c, elo, ehi, d1));
     HIPCHK(nemo::stage_window(c, elo, ehi, d1));
@@ -379,11 +394,11 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
       HIPCHK(dalloc(&c.d_pwpos, ppos.size()));
       if (!c.d_xqueue) HIPCHK(dalloc(&c.d_xqueue, 1));
       HIPCHK(dalloc(&c.d_xbits, bits.size()));
-      HIPCHK(hipMemcpy(c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(c.d_pwplan, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(c.d_pwpos, ppos.data(), ppos.size() * 4, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(c.d_xbits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_pwplan, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_pwpos, ppos.data(), ppos.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_xbits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
       c.pw_ns = pl.ns;
       c.pw_nh = pl.nh;
       c.pw_maxrem = pl.maxrem;
@@ -407,8 +422,11 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
 
 extern "C" {
 
+// Staging takes no process-wide lock: its copies and fills run on the
+// context's own non-blocking stream (nemo::copy_sync), so they neither touch
+// the legacy stream nor wait for another engine's capture
+// (tests/test_gpu_parity.py::test_staging_while_another_engine_captures)
 int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
-  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!U || !T) return fail(NEMO_ERR_ARG, "null table");
@@ -447,7 +465,7 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
   }
   HIPCHK(hipStreamSynchronize(c.stream));
   HIPCHK(hipFree(d_t64));
-  HIPCHK(hipMemcpy(c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
+  HIPCHK(nemo::copy_sync(c, c.d_U64, U, (S + 1) * E * 8, hipMemcpyHostToDevice));
   c.table_absmax = amax;
 
   // factored form: every off-diagonal row T[.][j] identical for all children
@@ -463,7 +481,6 @@ int nemo_stage_tables(nemo_ctx* ctx, const double* U, const double* T) {
 }
 
 int nemo_stage_knockdown(nemo_ctx* ctx, const uint8_t* D, double A, double B) {
-  NEMO_API_LOCK;
   int rc = check_ctx(ctx, false);
   if (rc) return rc;
   if (!D) return fail(NEMO_ERR_ARG, "null knockdown matrix");
@@ -1285,7 +1302,7 @@ int nemo_fetch_exact_trace(nemo_ctx* ctx, int* n, long long* out) {
   HIPCHK(hipStreamSynchronize(c.stream));
   *n = c.xtrace_n;
   if (out && c.xtrace_n > 0)
-    HIPCHK(hipMemcpy(out, c.d_xtrace, (size_t)c.xtrace_n * 4 * sizeof(long long), hipMemcpyDeviceToHost));
+    HIPCHK(nemo::copy_sync(c, out, c.d_xtrace, (size_t)c.xtrace_n * 4 * sizeof(long long), hipMemcpyDeviceToHost));
   return NEMO_OK;
 }
 
@@ -1474,6 +1491,11 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     ctx->c.anc_overlap = value ? 1 : 0;
     return NEMO_OK;
   }
+  if (strcmp(name, "timing_kernel") == 0) {
+    if (value < 0 || value > 1) return fail(NEMO_ERR_ARG, "timing_kernel %d (0 score kernels, 1 exact local optima)", value);
+    ctx->c.timing_kernel = value;
+    return NEMO_OK;
+  }
   if (strcmp(name, "exact_persist") == 0) {
     ctx->c.exact_persist = value ? 1 : 0;
     return NEMO_OK;
@@ -1554,6 +1576,7 @@ int nemo_get_option(nemo_ctx* ctx, const char* name, int* value) {
   else if (strcmp(name, "exact_xcd") == 0) *value = c.exact_xcd;
   else if (strcmp(name, "exact_trace") == 0) *value = c.exact_trace;
   else if (strcmp(name, "exact_persist") == 0) *value = c.exact_persist;
+  else if (strcmp(name, "timing_kernel") == 0) *value = c.timing_kernel;
   else if (strcmp(name, "exact_sched") == 0) *value = c.exact_sched;
   else if (strcmp(name, "anc_overlap") == 0) *value = c.anc_overlap;
   else if (strcmp(name, "exact_lat_waves") == 0) *value = c.exact_lat_waves;

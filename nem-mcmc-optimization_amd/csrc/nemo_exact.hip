@@ -1474,6 +1474,13 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
     a.ca.order = c.d_xorder;
   }
   const dim3 grid(lo_blocks + fin_blocks);
+  hipEvent_t e0 = nullptr, e1 = nullptr;   // (option timing_kernel 1: bench.py's local-optimum roofline)
+  if (c.timing && c.timing_kernel == 1 && c.ev_used + 2 <= c.ev_pool.size()) {
+    e0 = c.ev_pool[c.ev_used++];
+    e1 = c.ev_pool[c.ev_used++];
+    const hipError_t re = hipEventRecord(e0, st);
+    if (re != hipSuccess) return re;
+  }
   if (form == 5) a.ca.trace = nullptr;   // (the dual form keeps no timeline)
   c.xtrace_n = a.ca.trace ? nw : 0;
   switch (c.pw_ns) {
@@ -1486,6 +1493,11 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
     case 7: launch_lo_ns<7>(a, form, rc, grid, st); break;
     case 8: launch_lo_ns<8>(a, form, rc, grid, st); break;
     default: return hipErrorInvalidValue;
+  }
+  if (e1) {
+    const hipError_t re = hipEventRecord(e1, st);
+    if (re != hipSuccess) return re;
+    ++c.launches;
   }
   return hipGetLastError();
 }

@@ -663,7 +663,7 @@ hipError_t launch_score_factored(Ctx& c, int batch, int cap, const int32_t* d_po
   }
   if (err != hipSuccess) return err;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+  if (c.timing && c.timing_kernel == 0 && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
     { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }

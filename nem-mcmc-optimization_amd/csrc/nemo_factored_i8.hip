@@ -2151,7 +2151,7 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
   hipError_t err = hipStreamSynchronize(c.stream);
   if (err != hipSuccess) return err;
   std::vector<double> U((size_t)(S + 1) * E);
-  if ((err = hipMemcpy(U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
+  if ((err = copy_sync(c, U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
   const double* un = U.data() + (size_t)S * E;
   std::vector<double> uo((size_t)(SPAD + 1) * E + 16, 0.0);
   double umin = 0.0, umax = 0.0;
@@ -2201,7 +2201,7 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       lt[2 * k + 1] = (double)-logl((long double)inv);
     }
     if ((err = hipMalloc(&c.d_i8o_tabs, tb.size() * 4)) != hipSuccess) return err;
-    if ((err = hipMemcpy(c.d_i8o_tabs, tb.data(), tb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    if ((err = copy_sync(c, c.d_i8o_tabs, tb.data(), tb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
       return err;
   }
   // diagonal form: U'[i][e] = u0_i + (u1_i - u0_i) D1[i][e] (within 1e-11; every U
@@ -2270,8 +2270,8 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       expand(false, dig);
       if ((err = hipMalloc((void**)&c.d_udig, dig.size())) != hipSuccess) return err;
       if ((err = hipMalloc((void**)&c.d_u0, S * 8)) != hipSuccess) return err;
-      if ((err = hipMemcpy(c.d_udig, dig.data(), dig.size(), hipMemcpyHostToDevice)) != hipSuccess) return err;
-      if ((err = hipMemcpy(c.d_u0, u0.data(), S * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+      if ((err = copy_sync(c, c.d_udig, dig.data(), dig.size(), hipMemcpyHostToDevice)) != hipSuccess) return err;
+      if ((err = copy_sync(c, c.d_u0, u0.data(), S * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
       c.i8o_diag = true;
       // log2 fixed point: every entry v = delta 2^20 / ln 2 needs |rint(v)| <
       // 2^25 - 2^17 - 2^6 (top digit in [-128, 127] after the balancing bias),
@@ -2289,7 +2289,7 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       if (dmax * kL2Scale < vmax && (gabs + umax0) / kLn2 + 1023.0 < 2000.0 && -padg / kLn2 < 1000.0) {
         expand(true, dig2);
         if ((err = hipMalloc((void**)&c.d_udig2, dig2.size())) != hipSuccess) return err;
-        if ((err = hipMemcpy(c.d_udig2, dig2.data(), dig2.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        if ((err = copy_sync(c, c.d_udig2, dig2.data(), dig2.size(), hipMemcpyHostToDevice)) != hipSuccess)
           return err;
         c.i8l_ok = true;
       }
@@ -2306,14 +2306,14 @@ hipError_t stage_i8o(Ctx& c, const std::vector<double>& elo, const std::vector<d
       nw[s2] = acc;
     }
     if ((err = hipMalloc((void**)&c.d_nullsum_w, nw.size() * 8)) != hipSuccess) return err;
-    if ((err = hipMemcpy(c.d_nullsum_w, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
+    if ((err = copy_sync(c, c.d_nullsum_w, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
       return err;
     c.i8w_ok = true;
   }
   if ((err = hipMalloc((void**)&c.d_Uoff, uo.size() * 8)) != hipSuccess) return err;
   if ((err = hipMalloc((void**)&c.d_nullsum, ns.size() * 8)) != hipSuccess) return err;
-  if ((err = hipMemcpy(c.d_Uoff, uo.data(), uo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
-  if ((err = hipMemcpy(c.d_nullsum, ns.data(), ns.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = copy_sync(c, c.d_Uoff, uo.data(), uo.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = copy_sync(c, c.d_nullsum, ns.data(), ns.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
   c.i8o_padg = padg;
   c.i8o_ok = true;
   return hipSuccess;

@@ -216,8 +216,10 @@ struct Ctx {
   StepGraph step_graph[kStepGraphs];
   int step_graph_next = 0;
 
-  // timing of the score kernel
+  // timing of the score kernel (timing_kernel 0) or of the exact local
+  // optima's kernel (1; option "timing_kernel")
   bool timing = false;
+  int timing_kernel = 0;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   int launches = 0;
@@ -225,6 +227,15 @@ struct Ctx {
 
   int ntiles() const { return (E + kTileCols - 1) / kTileCols; }
 };
+
+// A staging copy on the context's own stream, finished on return (so the host
+// buffer may be freed or read): never on HIP's legacy stream, whose
+// operations HIP refuses while a blocking stream of the process captures, and
+// ordered with the staging kernels on c.stream
+inline hipError_t copy_sync(const Ctx& c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c.stream);
+  return e != hipSuccess ? e : hipStreamSynchronize(c.stream);
+}
 
 // the partial buffer the score kernels write (Ctx::part_out over d_fpartial)
 inline double* fpartial(const Ctx& c) { return c.part_out ? c.part_out : c.d_fpartial; }

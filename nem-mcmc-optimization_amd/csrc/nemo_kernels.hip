@@ -818,7 +818,7 @@ hipError_t launch_score(Ctx& c, int batch, const int32_t* d_rows, const double* 
   dim3 grid(nt * batch);
   const bool rn = needs_renorm(c);
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+  if (c.timing && c.timing_kernel == 0 && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
     { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }
@@ -887,7 +887,7 @@ static hipError_t launch_group_t(Ctx& c, int batch, hipStream_t st) {
 
 hipError_t launch_score_group(Ctx& c, int batch, int group, double* d_ll, hipStream_t st) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c.timing && c.ev_used + 2 <= c.ev_pool.size()) {
+  if (c.timing && c.timing_kernel == 0 && c.ev_used + 2 <= c.ev_pool.size()) {
     e0 = c.ev_pool[c.ev_used++];
     e1 = c.ev_pool[c.ev_used++];
     { hipError_t re = hipEventRecord(e0, st); if (re != hipSuccess) return re; }

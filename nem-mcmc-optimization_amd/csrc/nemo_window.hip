@@ -448,7 +448,7 @@ hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vecto
   hipError_t err = hipStreamSynchronize(c.stream);
   if (err != hipSuccess) return err;
   std::vector<double> U((size_t)(S + 1) * E);
-  if ((err = hipMemcpy(U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
+  if ((err = copy_sync(c, U.data(), c.d_U64, U.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return err;
   const double* un = U.data() + (size_t)S * E;
   std::vector<double> uw(2 * (size_t)S, 0.0);
   double umin = 0.0, umax = 0.0;
@@ -495,8 +495,8 @@ hipError_t stage_window(Ctx& c, const std::vector<double>& elo, const std::vecto
   }
   if ((err = hipMalloc((void**)&c.d_wuw, uw.size() * 8)) != hipSuccess) return err;
   if ((err = hipMalloc((void**)&c.d_wnull, nw.size() * 8)) != hipSuccess) return err;
-  if ((err = hipMemcpy(c.d_wuw, uw.data(), uw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
-  if ((err = hipMemcpy(c.d_wnull, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = copy_sync(c, c.d_wuw, uw.data(), uw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
+  if ((err = copy_sync(c, c.d_wnull, nw.data(), nw.size() * 8, hipMemcpyHostToDevice)) != hipSuccess) return err;
   c.win_ok = true;
   return hipSuccess;
 }

@@ -269,19 +269,25 @@ class Engine:
                                             C.byref(b)))
         return fk.value, b.value
 
-    def exact_status(self):
+    def exact_limits(self, cap: int = 0):
+        """The reference-arithmetic path's limits for this model
+        (``nemo.limits``: one row per limit, the model's value, whether it is
+        covered and what the sampler does outside it)."""
+        from .limits import exact_limits
+        return exact_limits(self.S, self.E, self.factored, cap, host_blas_arch(),
+                            exact_option=bool(self.get_option("exact")))
+
+    def exact_status(self, cap: int = 0):
         """(True, "") when the fused step and the sampler's score calls run in
         the reference's own arithmetic (option ``exact``, the default, on a
-        model the exact kernels cover); else (False, the reason)."""
-        if not self.get_option("exact"):
-            return False, "option exact is 0"
-        if not self.factored:
-            return False, ("the staged tables are not the factored form nem.py builds (every off-diagonal "
-                           "row shared by all children, two-valued)")
-        if not self.get_option("exact_ok"):
-            return False, (f"numpy's pairwise sum of E={self.E} effects needs more than 64 leaf blocks "
-                           "(the exact kernels' wave plan covers E <= 8192)")
-        return True, ""
+        model the exact kernels cover); else (False, the limit that breaks it
+        and what runs instead) -- the rows of ``exact_limits``."""
+        from .limits import exact_status_from
+        ok, why = exact_status_from(self.exact_limits(cap))
+        # the library's own verdict on the staging (the wave plan it built)
+        if ok and not self.get_option("exact_ok"):
+            return False, f"E={self.E}: the staging found no wave plan for numpy's pairwise sum; the fast kernels"
+        return ok, why
 
     @property
     def factored(self) -> bool:

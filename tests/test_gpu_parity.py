@@ -11,7 +11,7 @@ from conftest import golden
 from scipy.special import expit
 
 import nemo_oracle as no
-from nemo import NEM, generator, utils
+from nemo import NEM, _lib, generator, utils
 from nemo.engine import Engine, lse_full
 
 pytestmark = pytest.mark.gpu
@@ -834,6 +834,41 @@ def test_staging_while_the_gpu_is_busy():
                 e.close()
     finally:
         call.end()
+        busy.close()
+
+
+def test_staging_while_another_engine_captures():
+    """Staging takes no process-wide lock (its copies run on the context's own
+    stream): stage C2 engines on this thread while a busy C3
+    engine's step thread captures a new graph for every call (a new sig0 per
+    call misses the graph cache), with the library lock out of the staging
+    path.  Every staged engine scores the golden bits, every step returns
+    NEMO_OK, and no HIP error is left behind."""
+    from nemo.nem_order_mcmc import SIG0, SIG1
+    m3 = generator.config_nem("C3")
+    busy = Engine.for_nem(m3)
+    rng = np.random.default_rng(6)
+    n = 8
+    pos3 = np.array([np.argsort(rng.permutation(64)) for _ in range(n)], dtype=np.int32)
+    w3 = rng.uniform(-3, 3, (n, 64, 64))
+    m2 = generator.config_nem("C2")
+    perm = rng.permutation(16)
+    pos = np.argsort(perm)[None].astype(np.int32)
+    w01 = expit(rng.uniform(-3, 3, (1, 16, 16)))
+    ref = no.order_score(m2.U, m2.get_score_tensor(), perm, w01[0])
+    assert busy.get_option("graphs") == 1
+    try:
+        for k in range(12):
+            call = busy.bind_optimal_weights_w(pos3, w3, SIG0 + 1e-6 * (k + 1), SIG1, want_prep=False)
+            call.begin()
+            engs = [Engine.from_knockdown(m2.observed_knockdown_mat, m2.A, m2.B) for _ in range(2)]
+            call.end()
+            assert call.rc in (0, _lib.NEMO_ERR_OPT), _lib.load().nemo_last_error()
+            for e in engs:
+                assert abs(e.score(pos, w01)[0] - ref) <= 1e-9
+                e.close()
+        assert busy.get_option("graphs") == 1   # no capture failed (a failure turns graphs off)
+    finally:
         busy.close()
 
 
