@@ -294,8 +294,9 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                (cells built in d_ow -- then order weights in place -- or in
  *                d_cells, not both)
  *   "exact_ok"   (get only) 1 if the staging supports "exact" (factored
- *                tables, no parent cap, numpy's pairwise sum of E fits the
- *                wave plan)
+ *                tables, any parent cap, E <= 524288: numpy's np.sum adds
+ *                buffers of 8192 terms in order, each summed pairwise, and
+ *                the local optima run one wave plan per buffer)
  *   "exact_form" the exact local-optimum kernel's form (same bits): 0 auto
  *                (default: the latency form while chains x pairs <=
  *                "exact_lat_waves", 32768 by default = 16 C3 chains, the
@@ -304,7 +305,12 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                optimum, two per SIMD, the optimum's c values held in
  *                registers), 2 throughput (four per SIMD, c recomputed each
  *                evaluation), 3 pair (two waves per optimum, the objective's
- *                slots split between them; E > 1024)
+ *                slots split between them; E > 1024), 4 cached throughput
+ *                (three per SIMD, the cache partly in scratch), 5 dual (two
+ *                optima per wave, one per half; measured slower, DESIGN.md
+ *                3.5e); E > 8192 always runs the throughput form
+ *   "timing_kernel" 0 (default): nemo_timing_enable / _read time the score
+ *                kernels; 1: the exact local optima's kernel (bench.py)
  *   "anc_overlap" 1 (default): nemo_optimal_weights_w makes ancestor_x on a
  *                second stream beside eval #1 (same bits); 0 = in line */
 int nemo_set_option(nemo_ctx* ctx, const char* name, int value);

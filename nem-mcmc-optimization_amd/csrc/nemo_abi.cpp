@@ -186,7 +186,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_fpartial, c.d_B8, c.d_inv_list, c.d_Uoff, c.d_nullsum, c.d_i8o_tabs,
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
                   c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf,
-                  c.d_xa,   c.d_xbits, c.d_pwpos, c.d_xtrace, c.d_xqueue,
+                  c.d_xa,   c.d_xbits, c.d_pwpos, c.d_pwmeta, c.d_xtrace, c.d_xqueue,
                   c.d_xcost, c.d_xorder, c.d_xhist};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -366,42 +366,43 @@ int stage_factored(nemo_ctx* ctx, bool fact, const std::vector<uint64_t>& d1,
     // row (the reference's local_vec = np.exp(T[i][k]), restated bit for bit)
     // and the wave layout of numpy's pairwise sum of E terms
     c.exact_ok = false;
-    nemo::host::PairwisePlan pl;
-    if (nemo::host::build_pairwise_plan(c.E, pl) && pl.ns <= nemo::kExactMaxSlots && pl.nh <= 8) {
+    c.pw_parts = 1;
+    // numpy's pairwise sum of E as wave plans: one, or the two halves of its
+    // top split when E needs more than 64 leaf blocks (E > 8192)
+    std::vector<nemo::host::PairwisePlan> parts;
+    bool plan_ok = nemo::host::build_pairwise_parts(c.E, parts) && parts.size() <= (size_t)nemo::kExactMaxParts;
+    for (const auto& p : parts) plan_ok = plan_ok && p.ns <= nemo::kExactMaxSlots && p.nh <= 8;
+    if (plan_ok) {
       std::vector<double> xlo(S), xhi(S);
       for (size_t j = 0; j < S; ++j) {
         xlo[j] = nemo::refmath::svml_exp(tlo[j]);
         xhi[j] = nemo::refmath::svml_exp(thi[j]);
       }
-      // the partner rows padded to the 8 heights the kernels read (-1: none)
-      std::vector<int32_t> partner = pl.partner;
-      partner.resize((size_t)8 * 64, -1);
-      std::vector<int32_t> dev;
-      dev.insert(dev.end(), pl.start.begin(), pl.start.end());
-      dev.insert(dev.end(), pl.cnt.begin(), pl.cnt.end());
-      dev.insert(dev.end(), pl.rem.begin(), pl.rem.end());
-      dev.insert(dev.end(), pl.nrem.begin(), pl.nrem.end());
-      dev.insert(dev.end(), partner.begin(), partner.end());
+      std::vector<int32_t> dev, meta;
+      nemo::host::parts_device_rows(parts, dev, meta);
       // the recompute form's element -> plan position map and lv bits per
       // (parent row, slot, lane)
       std::vector<int32_t> ppos;
       std::vector<uint32_t> bits;
-      nemo::host::plan_positions(pl, ppos);
-      nemo::host::plan_lv_bits(pl, c.S, d1.data(), nwords, bits);
+      nemo::host::parts_positions(parts, c.E, ppos);
+      nemo::host::parts_lv_bits(parts, c.S, d1.data(), nwords, bits);
       HIPCHK(dalloc(&c.d_xlo, S));
       HIPCHK(dalloc(&c.d_xhi, S));
       HIPCHK(dalloc(&c.d_pwplan, dev.size()));
+      HIPCHK(dalloc(&c.d_pwmeta, meta.size()));
       HIPCHK(dalloc(&c.d_pwpos, ppos.size()));
       if (!c.d_xqueue) HIPCHK(dalloc(&c.d_xqueue, 1));
       HIPCHK(dalloc(&c.d_xbits, bits.size()));
       HIPCHK(nemo::copy_sync(c, c.d_xlo, xlo.data(), S * 8, hipMemcpyHostToDevice));
       HIPCHK(nemo::copy_sync(c, c.d_xhi, xhi.data(), S * 8, hipMemcpyHostToDevice));
       HIPCHK(nemo::copy_sync(c, c.d_pwplan, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(nemo::copy_sync(c, c.d_pwmeta, meta.data(), meta.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(nemo::copy_sync(c, c.d_pwpos, ppos.data(), ppos.size() * 4, hipMemcpyHostToDevice));
       HIPCHK(nemo::copy_sync(c, c.d_xbits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
-      c.pw_ns = pl.ns;
-      c.pw_nh = pl.nh;
-      c.pw_maxrem = pl.maxrem;
+      c.pw_ns = nemo::host::parts_slots(parts);
+      c.pw_parts = (int)parts.size();
+      c.pw_nh = parts[0].nh;
+      c.pw_maxrem = parts[0].maxrem;
       c.exact_ok = true;
     }
   }
@@ -828,7 +829,7 @@ int exact_reserve(Ctx& c, int nchains) {
       c.cap_xtrace = need;
     }
   }
-  if (c.exact_cform == 1) {
+  if (nemo::exact_rc(c)) {
     const size_t need = nc * S * plan;
     if (need > c.cap_xa) {
       ++c.graph_epoch;
@@ -885,13 +886,13 @@ int optimal_weights_enqueue(nemo_ctx* ctx, int nchains, const int32_t* d_pos, co
     // (eval #1's ll summed by the launch's appended blocks), eval #2 summed on
     // the device.  With a cap, the capped parent lists throughout (the prep's
     // pair lists, both evaluations' cells)
-    if (c.cap_xcells2 < (size_t)nchains || (c.exact_cform == 1 ? !c.d_xa : !c.d_xcbuf))
+    if (c.cap_xcells2 < (size_t)nchains || (nemo::exact_rc(c) ? !c.d_xa : !c.d_xcbuf))
       return fail(NEMO_ERR_STATE, "exact step buffers not reserved for %d chains", nchains);
     double* cs1 = c.d_xcs;
     double* cs2 = c.d_xcs + (size_t)nchains * c.E;
     HIPCHK(nemo::launch_step_prep(c, nchains, cap, d_pos, d_w01, d_info, st));
     HIPCHK(nemo::launch_exact_eval(c, nchains, cap, d_pos, d_w01, c.d_ow, cs1, nullptr, true, st,
-                                   c.exact_cform == 1 ? c.d_xa : nullptr));
+                                   nemo::exact_rc(c) ? c.d_xa : nullptr));
     if (anc_ready) HIPCHK(hipStreamWaitEvent(st, anc_ready, 0));  // ancestor_x from the second stream
     HIPCHK(nemo::launch_local_opt_exact(c, nchains, nemo::pairs_per_chain(c.S, cap), c.d_pairs, d_w01, d_anc, c.d_ow,
                                         sig0, sig1, d_w_new,

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // the same rounded operations -- so the objective reads 1.1 MB per chain
 // instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
 // starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false>
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
@@ -369,6 +369,13 @@ struct ExactObjective {
   bool pad_guard = false;
   const int32_t* pl;   // host::PairwisePlan rows in LDS: start, cnt, rem, nrem [NS][64], partner [8][64]
   int nh, maxrem, lane;
+  // numpy's pairwise sum in two wave plans (E > 8192, CArgs::nparts): each
+  // part's rows in global memory (plg), its height and trailing count (pmeta),
+  // kRc: the parent's lv bits of all parts' slots (xbk)
+  int nparts = 1;
+  const int32_t* plg = nullptr;
+  const int32_t* pmeta = nullptr;
+  const uint32_t* xbk = nullptr;
   double anc;
   LdsTabs tb;
 
@@ -473,23 +480,25 @@ struct ExactObjective {
   __device__ __forceinline__ void slot_sums(int u, double ex0, double ex1, double& a0, double& a1) const {
 #pragma clang fp contract(off)
     const int cu = cnt(u);
-    a0 = 0.0;
-    a1 = 0.0;
+    // the chain starts from -0.0: -0.0 + t is t for every t, so the first term
+    // is added like the rest -- the same bits as starting from it, without a
+    // select per term where the loop index is not a constant (the throughput
+    // form's unroll by 4)
+    a0 = -0.0;
+    a1 = -0.0;
     // past the chain's count c is 0 (the rows are written so; cval gives 0),
     // so its term is log(0 ex + 1) = +0 and a + 0 = a: a is never -0 (a log is
     // never -0, and a sum of nonzero terms rounds to +0), so no select is needed
-    auto step = [&](int m, double cm) {
+    auto step = [&](int, double cm) {
       double t0, t1;
       log_pair(cm * ex0 + 1.0, cm * ex1 + 1.0, t0, t1);
-      if (m == 0) {
-        a0 = t0;
-        a1 = t1;
-      } else {
-        a0 = a0 + t0;
-        a1 = a1 + t1;
-      }
+      a0 = a0 + t0;
+      a1 = a1 + t1;
     };
-    if (kLat || kCache) {   // (a cached c needs constant indices: a loop index would put it in scratch)
+    // (the cached throughput form keeps the unroll by 4: its cache then lives
+    // in scratch, which measured faster than registers at its 3-wave budget --
+    // 1.61 against 1.84 ms per 16-chain step, profiles/r6/r6f_forms_sweep.txt)
+    if (kLat) {
       double c[kChain];
 #pragma unroll
       for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
@@ -579,12 +588,45 @@ struct ExactObjective {
         res0[u] = xr[(u * kWave + lane) * 2];
         res1[u] = xr[(u * kWave + lane) * 2 + 1];
       }
-    } else {
+    } else if (!kMP) {
 #pragma unroll
       for (int u = 0; u < NS; ++u) {
         if (kLat && u > 0) __asm__ volatile("" ::: "memory");   // one slot's c loaded at a time
         slot_sums(u, ex0, ex1, res0[u], res1[u]);
       }
+    } else {
+      // numpy's buffers of 8192 terms (E > 8192), each summed pairwise on
+      // its own wave plan and added to the running sum in order
+      const int32_t* pl0 = pl;
+      const double* cp0 = cp;
+      const int nh0 = nh, mr0 = maxrem;
+      double q0 = 0.0, q1 = 0.0;
+      for (int p = 0; p < nparts; ++p) {
+        pl = plg + (size_t)p * (4 * NS + 8) * kWave;
+        nh = pmeta[2 * p];
+        maxrem = pmeta[2 * p + 1];
+        if (kPlan) cp = cp0 + (size_t)p * NS * kRows * kWave;
+        if (kRc) {
+#pragma unroll
+          for (int u = 0; u < NS; ++u) rbits[kRc ? u : 0] = xbk[((size_t)p * NS + u) * kWave + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
+          __asm__ volatile("" ::: "memory");
+          slot_sums(u, ex0, ex1, res0[u], res1[u]);
+        }
+        double p0, p1;
+        tree(res0, res1, p0, p1);
+        q0 = p == 0 ? p0 : q0 + p0;
+        q1 = p == 0 ? p1 : q1 + p1;
+      }
+      pl = pl0;
+      cp = cp0;
+      nh = nh0;
+      maxrem = mr0;
+      s0 = q0;
+      s1 = q1;
+      return;
     }
     tree(res0, res1, s0, s1);
   }
@@ -632,6 +674,14 @@ struct CArgs {
   int* queue = nullptr;              // option exact_persist: the work counter (zeroed before the launch)
   const int32_t* order = nullptr;    // the optima in the order they are handed out (null: launch order)
   int32_t* cost = nullptr;           // option exact_sched: [chains][S][S] each pair's last evaluation count
+  // numpy's pairwise sum in nparts wave plans (two: the halves of its top
+  // split, E > 8192): the plans' rows in global memory, [part][2] (tree
+  // height, largest trailing count), and the doubles of one plan-ordered row
+  // set over all parts
+  int nparts = 1;
+  const int32_t* plan = nullptr;
+  const int32_t* pmeta = nullptr;
+  size_t pd = 0;
 };
 
 // The persistent form (option exact_persist): resident blocks whose waves take
@@ -650,11 +700,12 @@ __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E,
                                         double lvlo, double lvhi, const double* __restrict__ owk,
                                         const uint64_t* __restrict__ d1w, int nwords, int lane, unsigned slots) {
 #pragma clang fp contract(off)
-  constexpr size_t kPlanD = (size_t)NS * Obj::kRows * kWave;
+  constexpr size_t kPlanD = (size_t)NS * Obj::kRows * kWave;   // (one part: the stored form)
   if (kRc) {
-    obj.cp = ca.xa + ((size_t)b * S + k) * kPlanD;
+    obj.cp = ca.xa + ((size_t)b * S + k) * ca.pd;
+    obj.xbk = ca.xbits + (size_t)k * NS * ca.nparts * kWave;
 #pragma unroll
-    for (int u = 0; u < NS; ++u) obj.rbits[kRc ? u : 0] = ca.xbits[((size_t)k * NS + u) * kWave + lane];
+    for (int u = 0; u < NS; ++u) obj.rbits[kRc ? u : 0] = obj.xbk[(size_t)u * kWave + lane];
     obj.rs = s;
     obj.rslo = s * (lvlo - 1.0);
     obj.rshi = s * (lvhi - 1.0);
@@ -686,7 +737,7 @@ __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E,
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
 // kCt (form 4, the cached throughput form): the throughput form's objective
 // loop on the latency form's register c cache, at NEMO_EXACT_CT_WAVES per SIMD
-template <int NS, bool kLat, bool kRc, bool kCt = false>
+template <int NS, bool kLat, bool kRc, bool kCt = false, bool kMP = false>
 __global__ __launch_bounds__(kExactWaves * kWave)
 __attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES,
                                    kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
@@ -729,7 +780,7 @@ __attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_E
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -739,6 +790,9 @@ __attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_E
   obj.anc = anc[idx];
   obj.load_plan();
   setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
+  obj.nparts = ca.nparts;
+  obj.plg = ca.plan;
+  obj.pmeta = ca.pmeta;
   obj.fill_cache();
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, s);
@@ -1030,7 +1084,7 @@ __global__ __launch_bounds__(kExactWaves * kWave) __attribute__((amdgpu_waves_pe
   __syncthreads();
   const int hf = lane >> 5;
   const int total = nchains * npairs;
-  constexpr size_t kPlanD = (size_t)NS * DualObjective<NS>::kRows * kWave;
+  const size_t kPlanD = ca.pd;   // (one part: the dual form is not taken for two)
   DualObjective<NS> obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -1117,11 +1171,14 @@ __global__ __launch_bounds__(kExactWaves * kWave) __attribute__((amdgpu_waves_pe
 // the same optimiser on caller-supplied c vectors [n][E] (nemo_local_opt:
 // calculate_local_optimum of one pair, and the scipy records of the tests);
 // out [n][3] = x*, f*, packed info
-template <int NS>
+// (kMP: numpy's pairwise sum in two wave plans, E > 8192 -- the objective
+// reads each part's plan from global memory, nparts / pmeta as CArgs)
+template <int NS, bool kMP = false>
 __global__ __launch_bounds__(kExactWaves * kWave)
 __attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_generic_kernel(
     int E, int n, const double* __restrict__ cvec, const double* __restrict__ anc, const double* __restrict__ x0,
-    const int32_t* __restrict__ plan, int nh, int maxrem, double* __restrict__ out) {
+    const int32_t* __restrict__ plan, int nh, int maxrem, double* __restrict__ out, int nparts,
+    const int32_t* __restrict__ pmeta) {
 #pragma clang fp contract(off)
   __shared__ TabsLds tabs;
   __shared__ double mem[kExactWaves][lbx::kMemDoubles];
@@ -1134,7 +1191,7 @@ __attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_generic_kernel(
   const int p = __builtin_amdgcn_readfirstlane((int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave));
   const int lane = threadIdx.x & (kWave - 1);
   if (p >= n) return;
-  ExactObjective<NS, false, true> obj;
+  ExactObjective<NS, false, !kMP, false, false, false, kMP> obj;
   obj.tb = tabs.view();
   obj.pl = pl;
   obj.lane = lane;
@@ -1142,6 +1199,9 @@ __attribute__((amdgpu_waves_per_eu(2, 2))) void local_opt_exact_generic_kernel(
   obj.maxrem = maxrem;
   obj.anc = anc[p];
   obj.cp = cvec + (size_t)p * E;
+  obj.nparts = kMP ? nparts : 1;
+  obj.plg = plan;
+  obj.pmeta = pmeta;
   obj.load_plan();
   LbxState& st = *reinterpret_cast<LbxState*>(lst_raw[wv]);
   lbx_init(st, x0[p]);
@@ -1261,11 +1321,14 @@ hipError_t launch_local_opt_exact_generic(Ctx& c, int n, const double* d_c, cons
                                           double* d_out, hipStream_t st) {
   const dim3 grid((n + kExactWaves - 1) / kExactWaves);
   switch (c.pw_ns) {
-#define NEMO_EXACT_NS(NSV)                                                                                   \
-  case NSV:                                                                                                  \
-    local_opt_exact_generic_kernel<NSV><<<grid, kExactWaves * kWave, 0, st>>>(c.E, n, d_c, d_anc, d_x0,       \
-                                                                              c.d_pwplan, c.pw_nh,            \
-                                                                              c.pw_maxrem, d_out);            \
+#define NEMO_EXACT_NS(NSV)                                                                                  \
+  case NSV:                                                                                                 \
+    if (c.pw_parts > 1)                                                                                     \
+      local_opt_exact_generic_kernel<NSV, true><<<grid, kExactWaves * kWave, 0, st>>>(                      \
+          c.E, n, d_c, d_anc, d_x0, c.d_pwplan, c.pw_nh, c.pw_maxrem, d_out, c.pw_parts, c.d_pwmeta);       \
+    else                                                                                                    \
+      local_opt_exact_generic_kernel<NSV><<<grid, kExactWaves * kWave, 0, st>>>(                            \
+          c.E, n, d_c, d_anc, d_x0, c.d_pwplan, c.pw_nh, c.pw_maxrem, d_out, 1, c.d_pwmeta);                \
     break;
     NEMO_EXACT_NS(1)
     NEMO_EXACT_NS(2)
@@ -1289,7 +1352,9 @@ hipError_t launch_refmath_probe(int fn, int n, const double* d_x, const double* 
 
 bool exact_supported(const Ctx& c) { return c.factored && c.exact_ok && c.d_xlo && c.d_pwplan; }
 
-size_t exact_plan_doubles(const Ctx& c) { return (size_t)c.pw_ns * (ExactObjective<1, true, true>::kRows * kWave); }
+size_t exact_plan_doubles(const Ctx& c) {
+  return (size_t)c.pw_parts * c.pw_ns * (ExactObjective<1, true, true>::kRows * kWave);
+}
 
 hipError_t launch_exact_eval(Ctx& c, int batch, int cap, const int32_t* d_pos, const double* d_w01, double* d_cells,
                              double* d_cs, double* d_ll, bool want_ow, hipStream_t st, double* d_xa) {
@@ -1359,6 +1424,7 @@ int lo_resident(int form) {
   if (form == 3) return resident_blocks<local_opt_exact_pair_kernel<NS, kRc>>(2 * kWave);
   if (form == 1) return resident_blocks<local_opt_exact_kernel<NS, true, kRc>>(kExactWaves * kWave);
   if (form == 4) return resident_blocks<local_opt_exact_kernel<NS, false, kRc, true>>(kExactWaves * kWave);
+  if (form == 6) return resident_blocks<local_opt_exact_kernel<NS, false, true, false, true>>(kExactWaves * kWave);
   return resident_blocks<local_opt_exact_kernel<NS, false, kRc>>(kExactWaves * kWave);
 }
 
@@ -1379,6 +1445,10 @@ void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else if (form == 1)
     local_opt_exact_kernel<NS, true, kRc><<<grid, kExactWaves * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+  else if (form == 6)   // (internal: the throughput form on two plan parts)
+    local_opt_exact_kernel<NS, false, true, false, true><<<grid, kExactWaves * kWave, 0, st>>>(
         a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else if (form == 4)
@@ -1411,7 +1481,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
                                   double* d_wdag, int32_t* d_info, const double* d_cs1, double* d_ll1,
                                   hipStream_t st) {
   const int nw = nchains * npairs;
-  const bool rc = c.exact_cform == 1;
+  const bool rc = exact_rc(c);
   if (rc ? (size_t)nchains * c.S * exact_plan_doubles(c) > c.cap_xa
          : (size_t)nw * exact_plan_doubles(c) > c.cap_xcbuf)
     return hipErrorInvalidValue;
@@ -1425,6 +1495,9 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves && c.pw_ns <= 3)))
     form = 3;
   if (c.pw_ns < 2 && form == 3) form = 2;
+  // two plan parts (E > 8192): the throughput form, whose objective reads
+  // each part's plan from global memory and recomputes c per evaluation
+  if (c.pw_parts > 1) form = 6;
   // the persistent form: at most the resident blocks, the work counter zeroed
   const bool persist = c.exact_persist && c.d_xqueue;
   // the dual form (two optima per wave) needs the register cache's recompute
@@ -1482,6 +1555,10 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
     if (re != hipSuccess) return re;
   }
   if (form == 5) a.ca.trace = nullptr;   // (the dual form keeps no timeline)
+  a.ca.nparts = c.pw_parts;
+  a.ca.plan = c.d_pwplan;
+  a.ca.pmeta = c.d_pwmeta;
+  a.ca.pd = exact_plan_doubles(c);
   c.xtrace_n = a.ca.trace ? nw : 0;
   switch (c.pw_ns) {
     case 1: launch_lo_ns<1>(a, form, rc, grid, st); break;

@@ -131,7 +131,12 @@ struct PairwisePlan {
   std::vector<int32_t> start, cnt, rem, nrem, partner;
 };
 
-inline bool build_pairwise_plan(int E, PairwisePlan& pl) {
+// the plan of elements [off, off + n) (numpy's recursion on that range; the
+// plan's element indices are absolute)
+inline bool build_pairwise_plan_range(long off, long n, PairwisePlan& pl);
+inline bool build_pairwise_plan(int E, PairwisePlan& pl) { return build_pairwise_plan_range(0, E, pl); }
+
+inline bool build_pairwise_plan_range(long off, long E, PairwisePlan& pl) {
   struct Leaf { long s, n; };
   std::vector<Leaf> leaves;
   struct Op { int h, lane, partner; };
@@ -151,9 +156,9 @@ inline bool build_pairwise_plan(int E, PairwisePlan& pl) {
     return {l.first, h};
   };
   if (E < 1) return false;
-  const int root_h = rec(0, E).second;
+  const int root_h = rec(off, E).second;
   pl = PairwisePlan{};
-  pl.E = E;
+  pl.E = (int)(off + E);
   pl.nleaf = (int)leaves.size();
   if (pl.nleaf > 64) return false;  // one leaf result per lane for the tree
   pl.ns = (8 * pl.nleaf + 63) / 64;
@@ -184,6 +189,59 @@ inline bool build_pairwise_plan(int E, PairwisePlan& pl) {
   return true;
 }
 
+// np.sum of more than 8192 terms: numpy's reduction runs its inner loop on
+// buffer-sized chunks (np.getbufsize() = 8192 by default), each summed
+// pairwise and added to the running result in order -- sum = ((pw(c0) +
+// pw(c1)) + pw(c2)) + ..., measured against numpy 2.2 (tools/mp_probe.py,
+// DESIGN.md 3.5e).  Each chunk of <= 8192 terms fits one wave plan (<= 64
+// leaf blocks), so E takes ceil(E / 8192) plans with absolute element
+// indices.  One part when E <= 8192.
+constexpr long kNumpyBufsize = 8192;
+inline bool build_pairwise_parts(int E, std::vector<PairwisePlan>& parts, int max_parts = 64) {
+  parts.clear();
+  if (E < 1) return false;
+  const long np = (E + kNumpyBufsize - 1) / kNumpyBufsize;
+  if (np > max_parts) return false;
+  parts.assign((size_t)np, PairwisePlan{});
+  for (long p = 0; p < np; ++p) {
+    const long off = p * kNumpyBufsize, n = std::min<long>(kNumpyBufsize, E - off);
+    if (!build_pairwise_plan_range(off, n, parts[(size_t)p])) {
+      parts.clear();
+      return false;
+    }
+  }
+  return true;
+}
+
+// the parts' device rows, each padded to nsp slots: per part [start | cnt |
+// rem | nrem] x [nsp][64] then partner [8][64] (-1: none); meta [part][2] =
+// (tree height, largest trailing count)
+inline int parts_slots(const std::vector<PairwisePlan>& parts) {
+  int nsp = 0;
+  for (const auto& p : parts) nsp = std::max(nsp, p.ns);
+  return nsp;
+}
+inline void parts_device_rows(const std::vector<PairwisePlan>& parts, std::vector<int32_t>& dev,
+                              std::vector<int32_t>& meta) {
+  const int nsp = parts_slots(parts);
+  dev.clear();
+  meta.clear();
+  for (const auto& p : parts) {
+    auto pad = [&](const std::vector<int32_t>& v, int32_t fill) {
+      for (int u = 0; u < nsp; ++u)
+        for (int l = 0; l < 64; ++l) dev.push_back(u < p.ns ? v[(size_t)u * 64 + l] : fill);
+    };
+    pad(p.start, -1);
+    pad(p.cnt, 0);
+    pad(p.rem, -1);
+    pad(p.nrem, 0);
+    for (int h = 0; h < 8; ++h)
+      for (int l = 0; l < 64; ++l) dev.push_back(h < p.nh ? p.partner[(size_t)h * 64 + l] : -1);
+    meta.push_back(p.nh);
+    meta.push_back(p.maxrem);
+  }
+}
+
 // Where each element e sits in a plan-ordered row set ([ns][17][64] doubles:
 // chain element m of slot u on lane l at (u * 17 + m) * 64 + l, the lane's
 // trailing element at row 16): pos[e], every e < E exactly once.
@@ -212,6 +270,35 @@ inline void plan_lv_bits(const PairwisePlan& pl, int S, const uint64_t* d1, int 
         if (pl.rem[q] >= 0) w |= bit(k, pl.rem[q]) << 16;
         bits[((size_t)k * pl.ns + u) * 64 + l] = w;
       }
+}
+
+// plan_positions / plan_lv_bits over parts: part p's slot u is slot p nsp + u
+inline void parts_positions(const std::vector<PairwisePlan>& parts, int E, std::vector<int32_t>& pos) {
+  const int nsp = parts_slots(parts);
+  pos.assign((size_t)E, -1);
+  for (size_t p = 0; p < parts.size(); ++p) {
+    const PairwisePlan& pl = parts[p];
+    for (int u = 0; u < pl.ns; ++u)
+      for (int l = 0; l < 64; ++l) {
+        const size_t q = (size_t)u * 64 + l;
+        const int gu = (int)p * nsp + u;
+        for (int m = 0; m < pl.cnt[q]; ++m) pos[(size_t)pl.start[q] + 8 * m] = (gu * 17 + m) * 64 + l;
+        if (pl.rem[q] >= 0) pos[(size_t)pl.rem[q]] = (gu * 17 + 16) * 64 + l;
+      }
+  }
+}
+inline void parts_lv_bits(const std::vector<PairwisePlan>& parts, int S, const uint64_t* d1, int nwords,
+                          std::vector<uint32_t>& bits) {
+  const int nsp = parts_slots(parts), ns = (int)parts.size() * nsp;
+  bits.assign((size_t)S * ns * 64, 0u);
+  for (size_t p = 0; p < parts.size(); ++p) {
+    std::vector<uint32_t> b;
+    plan_lv_bits(parts[p], S, d1, nwords, b);
+    for (int k = 0; k < S; ++k)
+      for (int u = 0; u < parts[p].ns; ++u)
+        for (int l = 0; l < 64; ++l)
+          bits[((size_t)k * ns + p * nsp + u) * 64 + l] = b[((size_t)k * parts[p].ns + u) * 64 + l];
+  }
 }
 
 // the two addition chains of compute_scores (nem.py:25-34), in its order:

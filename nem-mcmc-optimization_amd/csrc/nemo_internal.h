@@ -21,7 +21,8 @@ constexpr int kFactWaves = 8;      // waves per factored-score block (16 effects
 constexpr int kI8MaxPairs = 5;     // digit-slice pairs of the int8 factored kernel
 constexpr int kWinMaxCap = 6;      // capped lookup-table kernel: parents per child
 constexpr int kWinMaxS = kMaxS;    // ... and S (LDS: ~356 S bytes per block)
-constexpr int kExactMaxSlots = 8;  // exact local optima: numpy's pairwise sum of E in <= 64 leaf blocks (E <= 8192)
+constexpr int kExactMaxSlots = 8;  // exact local optima: numpy's pairwise sum of E in <= 64 leaf blocks per part
+constexpr int kExactMaxParts = 64; // ... per numpy buffer of 8192 terms, 64 of them (E <= 524288)
 
 // Device state of one staged model on one GPU.
 struct Ctx {
@@ -131,8 +132,9 @@ struct Ctx {
   bool exact_ok = false;
   double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
   double* d_xhi = nullptr;         // [S] numpy's exp(hi_j)
-  int32_t* d_pwplan = nullptr;     // host::PairwisePlan of E, device layout
-  int pw_ns = 0, pw_nh = 0, pw_maxrem = 0;
+  int32_t* d_pwplan = nullptr;     // host::PairwisePlan of E (pw_parts of them, pw_ns slots each), device layout
+  int32_t* d_pwmeta = nullptr;     // [pw_parts][2]: each part's tree height and largest trailing count
+  int pw_ns = 0, pw_nh = 0, pw_maxrem = 0, pw_parts = 1;
   double* d_xcs = nullptr;         // [2][chains][E] cs of the step's two evaluations
   double* d_xcells2 = nullptr;     // [chains][S+1][E] eval #2's cells (allocated on first use)
   size_t cap_xcells2 = 0;          // its chains
@@ -286,6 +288,9 @@ hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const doub
 // the reference's arithmetic (nemo_exact.hip): supported for this staging?
 bool exact_supported(const Ctx& c);
 size_t exact_plan_doubles(const Ctx& c);   // one plan-ordered row set (per optimum / per parent row)
+// the local optima recompute c from the parents' a rows (option exact_cform 1,
+// and always for a plan in two parts, which the stored rows do not serve)
+inline bool exact_rc(const Ctx& c) { return c.exact_cform == 1 || c.pw_parts > 1; }
 // eval in the reference's order: cells into d_cells [batch][S+1][E] (with
 // want_ow: replaced by the order weights), cs into d_cs [batch][E], ll into
 // d_ll (nullable: left to the caller)

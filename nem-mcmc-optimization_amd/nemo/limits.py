@@ -16,12 +16,28 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 # the exact local optima's wave plan: one leaf block result per lane, the
-# leaves of numpy's pairwise recursion of E (csrc/nemo_host.h build_pairwise_plan)
+# leaves of numpy's pairwise recursion of one buffer of E (csrc/nemo_host.h
+# build_pairwise_plan; one plan per numpy buffer of 8192 terms)
 MAX_LEAVES = 64
 # the device's getrf / getri restatement (csrc/nemo_ancestor.hip)
 MAX_S_DEVICE_ANCESTOR = 64
 # the fast local optima (option exact 0)
 MAX_E_FAST_LOCAL_OPT = 80 * 64
+
+
+NUMPY_BUFSIZE = 8192      # np.getbufsize(): np.sum adds buffer-sized chunks in order
+MAX_PARTS = 64            # csrc/nemo_internal.h kExactMaxParts
+
+
+def pairwise_parts(E: int):
+    """The wave plans the exact local optima sum E terms in, as numpy's np.sum
+    does (csrc/nemo_host.h build_pairwise_parts): one per numpy buffer of
+    8192 terms, each summed pairwise, the chunks added in order; None past
+    MAX_PARTS buffers."""
+    if E < 1:
+        return None
+    parts = [min(NUMPY_BUFSIZE, E - k) for k in range(0, E, NUMPY_BUFSIZE)]
+    return parts if len(parts) <= MAX_PARTS else None
 
 
 def pairwise_leaves(E: int) -> int:
@@ -56,6 +72,7 @@ def exact_limits(S: int, E: int, factored: bool, cap: int = 0, host_blas: str | 
                  exact_option: bool = True) -> list[Limit]:
     """The exact path's limits for a model of S S-genes and E effects."""
     leaves = pairwise_leaves(E)
+    parts = pairwise_parts(E)
     rows = [
         Limit("option exact", "1 (default)", "1" if exact_option else "0", bool(exact_option),
               "the fast kernels: scores within ~1e-9, a local optimum may take another line-search path",
@@ -63,8 +80,11 @@ def exact_limits(S: int, E: int, factored: bool, cap: int = 0, host_blas: str | 
         Limit("table form", "factored: every off-diagonal row T[.][j] shared by all children, two-valued "
               "(every table nem.py builds)", "factored" if factored else "generic", bool(factored),
               "ExactArithmeticWarning (strict=True: RuntimeError); the fast kernels", False),
-        Limit("E (effects)", f"numpy's pairwise sum of E in <= {MAX_LEAVES} leaf blocks (E <= 8192)",
-              f"E={E}: {leaves} leaves", leaves <= MAX_LEAVES,
+        Limit("E (effects)", f"np.sum of E terms in <= {MAX_PARTS} numpy buffers of {NUMPY_BUFSIZE} (E <= "
+              f"{MAX_PARTS * NUMPY_BUFSIZE}; each buffer summed pairwise in <= {MAX_LEAVES} leaf blocks, the "
+              "buffers in order) -- with numpy's default np.getbufsize()",
+              f"E={E}: {leaves} leaves" + (f", {len(parts)} buffers" if parts and len(parts) > 1 else ""),
+              parts is not None,
               "ExactArithmeticWarning (strict=True: RuntimeError); the fast kernels"
               + ("" if E <= MAX_E_FAST_LOCAL_OPT else f" -- which take E <= {MAX_E_FAST_LOCAL_OPT}: the step fails"),
               False),

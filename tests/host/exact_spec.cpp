@@ -139,10 +139,30 @@ extern "C" {
 // host::build_pairwise_plan run as the device runs it (nemo_exact.hip's
 // ExactObjective::sum_logs, lanes as arrays): numpy's pairwise sum of a[E]?
 // Returns the sum, or NaN when the plan does not fit.
+static double plan_sum(const nemo::host::PairwisePlan& pl, const double* a);
+
 double spec_plan_sum(int E, const double* a) {
-#pragma clang fp contract(off)
   nemo::host::PairwisePlan pl;
   if (!nemo::host::build_pairwise_plan(E, pl)) return __builtin_nan("");
+  return plan_sum(pl, a);
+}
+
+// np.sum past one numpy buffer (E > 8192): the parts' plans, each run as the
+// wave runs it, added in order (host::build_pairwise_parts)
+double spec_parts_sum(int E, const double* a) {
+#pragma clang fp contract(off)
+  std::vector<nemo::host::PairwisePlan> parts;
+  if (!nemo::host::build_pairwise_parts(E, parts)) return __builtin_nan("");
+  double s = 0.0;
+  for (size_t p = 0; p < parts.size(); ++p) {
+    const double v = plan_sum(parts[p], a);
+    s = p == 0 ? v : s + v;
+  }
+  return s;
+}
+
+static double plan_sum(const nemo::host::PairwisePlan& pl, const double* a) {
+#pragma clang fp contract(off)
   const int NS = pl.ns;
   std::vector<double> res((size_t)NS * 64);
   for (int u = 0; u < NS; ++u) {

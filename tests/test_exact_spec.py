@@ -37,6 +37,7 @@ def spec(tmp_path_factory):
     lib.spec_objective.argtypes = [ctypes.c_int, _dp, ctypes.c_double, ctypes.c_double]
     lib.spec_eval.restype = ctypes.c_double
     lib.spec_plan_sum.restype = ctypes.c_double
+    lib.spec_parts_sum.restype = ctypes.c_double
     lib.spec_pairwise_sum.restype = ctypes.c_double
     return lib
 
@@ -134,6 +135,20 @@ def test_pairwise_sum_and_its_wave_plan(spec):
         ref = np.sum(a)
         assert spec.spec_pairwise_sum(ctypes.c_long(e), _p(a)) == ref, e
         assert spec.spec_plan_sum(e, _p(a)) == ref, e
+
+
+def test_np_sum_past_one_buffer_in_plan_parts(spec):
+    """np.sum of more than 8192 terms adds numpy's buffer-sized chunks (8192,
+    np.getbufsize()) in order, each summed pairwise -- not the pairwise
+    recursion over all E: the device's
+    parts (host::build_pairwise_parts, one wave plan per buffer) give numpy's
+    bits for E past 8192, up to 64 buffers."""
+    assert np.getbufsize() == 8192
+    rng = np.random.default_rng(6)
+    for e in (8192, 8193, 9000, 12345, 16384, 16385, 20000, 40000, 65536, 100001):
+        a = rng.normal(size=e) * np.exp(rng.normal(size=e) * 4)
+        assert spec.spec_parts_sum(e, _p(a)) == np.sum(a), e
+        assert spec.spec_parts_sum(e, _p(a)) == np.add.reduce(a), e
 
 
 @pytest.mark.parametrize("name", ["net2_200", "C2_20"])

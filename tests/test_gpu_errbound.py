@@ -65,9 +65,15 @@ def test_c3_auto_takes_log2_kernel_within_budget():
 
 @pytest.fixture(scope="module")
 def wide():
-    """64 S-genes x 16000 effects: 8x the headline's effects."""
+    """64 S-genes x 16000 effects: 8x the headline's effects.  The host-pointer
+    score calls here test the fixed-point kernels' error budget, so option
+    exact is 0 (E = 16000 is inside the exact path since round 6: numpy's
+    pairwise sum in four plan parts)."""
     m = generator.synthetic_nem(64, 16000, 0)
-    return m, Engine.for_nem(m), m.get_score_tensor()
+    eng = Engine.for_nem(m)
+    assert eng.get_option("exact_ok") == 1
+    eng.set_option("exact", 0)
+    return m, eng, m.get_score_tensor()
 
 
 def test_wide_model_auto_leaves_log2_kernel(wide):

@@ -189,12 +189,15 @@ def test_exact_fused_step_equals_oracle_c3():
     eng.close()
 
 
-@pytest.mark.parametrize("e", [2600, 3900, 4096, 4097, 5000])
+@pytest.mark.parametrize("e", [2600, 3900, 4096, 4097, 5000, 9000, 16384, 16392, 40000])
 def test_exact_fused_step_equals_oracle_more_slots(e):
     """E past 2048 (more than 16 leaf blocks of numpy's pairwise sum: 3 to 8
-    slots of the wave plan; 3900 and 4097 split into 33 leaves, 5000 into 64):
-    one fused step in the throughput and the pair forms, with c stored and
-    recomputed, against the oracle, to the bit."""
+    slots of the wave plan; 3900 and 4097 split into 33 leaves, 5000 into 64;
+    from 8193 numpy's np.sum adds buffers of 8192 terms, one wave plan each:
+    9000 and 16384 in two, 16392 in three, 40000 in five): one
+    fused step in the throughput
+    and the pair forms, with c stored and recomputed, against the oracle, to
+    the bit (several plans always take the throughput form, c recomputed)."""
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m = generator.synthetic_nem(12, e, 3)
     eng = Engine.for_nem(m)
@@ -394,26 +397,23 @@ def test_exact_chain_batch_equals_single_chains():
 
 
 def test_exact_fallback_is_loud():
-    """A model outside the exact kernels (E = 9000: numpy's pairwise sum in 128
-    leaf blocks; generic, non-factored tables) reports exact_ok 0, and the
-    sampler says so: a warning, or with strict=True an error.  A covered model
-    constructs silently."""
+    """A model outside the exact kernels (generic, non-factored tables)
+    reports exact_ok 0, and the sampler says so: a warning, or with
+    strict=True an error.  A covered model constructs silently -- E past 8192
+    included (numpy's buffers, one plan each)."""
     import warnings
     from nemo.engine import ExactArithmeticWarning
     from nemo.nem_order_mcmc import NEMOrderMCMC
-    m = generator.synthetic_nem(6, 9000, 1)
-    eng = Engine.for_nem(m)
-    assert eng.get_option("exact_ok") == 0 and eng.exact_status()[0] is False
-    perm = np.arange(6)
-    with pytest.warns(ExactArithmeticWarning, match="64 leaf blocks"):
-        NEMOrderMCMC(m, perm, engine=eng)
-    with pytest.raises(RuntimeError, match="fast kernels"):
-        NEMOrderMCMC(m, perm, engine=eng, strict=True)
-    eng.close()
+    big = Engine.for_nem(generator.synthetic_nem(3, 9000, 1))
+    assert big.get_option("exact_ok") == 1 and big.exact_status() == (True, "")
+    big.close()
     m = generator.synthetic_nem(6, 300, 1)
+    perm = np.arange(6)
     rng = np.random.default_rng(2)
     gen_eng = Engine(m.U, rng.normal(0, 1, (6, 6, 300)))   # not the factored form
     assert gen_eng.get_option("exact_ok") == 0
+    with pytest.warns(ExactArithmeticWarning, match="factored"):
+        NEMOrderMCMC(m, perm, engine=gen_eng)
     with pytest.raises(RuntimeError, match="factored"):
         NEMOrderMCMC(m, perm, engine=gen_eng, strict=True)
     gen_eng.close()

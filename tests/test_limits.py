@@ -16,6 +16,16 @@ def _numpy_leaves(E):
     return rec(E)
 
 
+def test_pairwise_parts_are_numpys_buffers():
+    # np.sum past 8192 terms: one plan per numpy buffer (tests/test_exact_spec.py
+    # checks the sums themselves against numpy)
+    assert limits.pairwise_parts(2000) == [2000] and limits.pairwise_parts(8192) == [8192]
+    assert limits.pairwise_parts(9000) == [8192, 808]
+    assert limits.pairwise_parts(16384) == [8192, 8192]
+    assert limits.pairwise_parts(64 * 8192) is not None and limits.pairwise_parts(64 * 8192 + 1) is None
+    assert all(limits.pairwise_leaves(n) <= limits.MAX_LEAVES for n in limits.pairwise_parts(100001))
+
+
 def test_pairwise_leaves_follow_numpys_recursion():
     for E in list(range(1, 300)) + [500, 1000, 2000, 3900, 4096, 4097, 5000, 8192, 8193, 8200, 9000, 16384]:
         assert limits.pairwise_leaves(E) == _numpy_leaves(E), E
@@ -36,9 +46,10 @@ def test_each_limit_on_both_sides():
     assert not ok and why.startswith("option exact")
     ok, why = _status(factored=False)
     assert not ok and why.startswith("table form")
-    assert _status(E=8192)[0] and not _status(E=9000)[0]
-    assert "E (effects)" in _status(E=9000)[1]
-    assert "the step fails" in _status(E=9000)[1]                    # past the fast local optima too
+    assert _status(E=8192)[0] and _status(E=9000)[0] and _status(E=100001)[0]   # buffers from 8193
+    assert not _status(E=64 * 8192 + 1)[0]                           # past 64 numpy buffers
+    assert "E (effects)" in _status(E=64 * 8192 + 1)[1]
+    assert "the step fails" in _status(E=64 * 8192 + 1)[1]           # past the fast local optima too
     for cap in (0, 1, 6, 63):
         assert _status(cap=cap)[0]
 
