@@ -299,8 +299,8 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                the local optima run one wave plan per buffer)
  *   "exact_form" the exact local-optimum kernel's form (same bits): 0 auto
  *                (default: the latency form while chains x pairs <=
- *                "exact_lat_waves", 32768 by default = 16 C3 chains, the
- *                throughput form beyond; the pair form while chains x pairs <=
+ *                "exact_lat_waves", 20000 by default ~ 10 C3 chains, the slot
+ *                form beyond; the pair form while chains x pairs <=
  *                "exact_pair_waves", 0 by default), 1 latency (one wave per
  *                optimum, two per SIMD, the optimum's c values held in
  *                registers), 2 throughput (four per SIMD, c recomputed each
@@ -308,7 +308,11 @@ int nemo_inverse_sweep(nemo_ctx* ctx, int nprob, const int32_t* pos, const doubl
  *                slots split between them; E > 1024), 4 cached throughput
  *                (three per SIMD, the cache partly in scratch), 5 dual (two
  *                optima per wave, one per half; measured slower, DESIGN.md
- *                3.5e); E > 8192 always runs the throughput form
+ *                3.5e), 7 slot (four per SIMD, c made once per optimum into
+ *                the resident wave's own row set in device memory, read at
+ *                each evaluation; needs "exact_cform" 1 and "exact_persist",
+ *                else the throughput form); E > 8192 always runs the
+ *                throughput form
  *   "timing_kernel" 0 (default): nemo_timing_enable / _read time the score
  *                kernels; 1: the exact local optima's kernel (bench.py)
  *   "anc_overlap" 1 (default): nemo_optimal_weights_w makes ancestor_x on a

@@ -187,7 +187,7 @@ void nemo_ctx_destroy(nemo_ctx* ctx) {
                   c.d_udig, c.d_udig2, c.d_u0, c.d_wuw, c.d_wnull, c.d_nullsum_w, c.d_i8img,
                   c.d_xlo,  c.d_xhi,  c.d_pwplan, c.d_xcs, c.d_xcells2, c.d_xcbuf,
                   c.d_xa,   c.d_xbits, c.d_pwpos, c.d_pwmeta, c.d_xtrace, c.d_xqueue,
-                  c.d_xcost, c.d_xorder, c.d_xhist};
+                  c.d_xcost, c.d_xorder, c.d_xhist, c.d_xsbuf};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < Ctx::kStepSlots; ++k) {
@@ -841,6 +841,14 @@ int exact_reserve(Ctx& c, int nchains) {
       c.cap_xa = need;
       grew = true;
     }
+    // the slot form's row sets (one plan part; a fixed size: its resident waves)
+    const size_t sneed = c.pw_parts == 1 ? nemo::exact_slot_doubles(c) : 0;
+    if (sneed > c.cap_xsbuf) {
+      ++c.graph_epoch;
+      HIPCHK(hipStreamSynchronize(c.stream));
+      HIPCHK(dalloc(&c.d_xsbuf, sneed));
+      c.cap_xsbuf = sneed;
+    }
   } else {
     const size_t need = nc * (size_t)nemo::pairs_per_chain(c.S, 0) * plan;
     if (need > c.cap_xcbuf) {
@@ -1469,9 +1477,10 @@ int nemo_set_option(nemo_ctx* ctx, const char* name, int value) {
     return NEMO_OK;
   }
   if (strcmp(name, "exact_form") == 0) {
-    if (value < 0 || value > 5)
+    if (value < 0 || value > 7 || value == 6)
       return fail(NEMO_ERR_ARG,
-                  "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair, 4 cached throughput, 5 dual)", value);
+                  "exact_form %d (0 auto, 1 latency, 2 throughput, 3 pair, 4 cached throughput, 5 dual, 7 slot)",
+                  value);
     ctx->c.exact_form = value;
     return NEMO_OK;
   }

@@ -37,6 +37,15 @@
 #ifndef NEMO_EXACT_TPUT_WAVES
 #define NEMO_EXACT_TPUT_WAVES 4   // the throughput form's waves per SIMD (its register budget)
 #endif
+#ifndef NEMO_EXACT_TPUT_UNROLL
+#define NEMO_EXACT_TPUT_UNROLL 4   // the throughput forms' chain loop unroll
+#endif
+#ifndef NEMO_EXACT_SLOT_WAVES
+#define NEMO_EXACT_SLOT_WAVES 4   // the slot form's waves per SIMD
+#endif
+#ifndef NEMO_EXACT_SLOT_PRE
+#define NEMO_EXACT_SLOT_PRE 0     // the slot form loads a slot's c values at once (ExactObjective::kPre)
+#endif
 #ifndef NEMO_EXACT_CT_WAVES
 #define NEMO_EXACT_CT_WAVES 3   // the cached throughput form's waves per SIMD (form 4)
 #endif
@@ -350,7 +359,10 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // the same rounded operations -- so the objective reads 1.1 MB per chain
 // instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
 // starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false>
+// kPre: the chain loop software pipelined (the next 4 elements' c loads in
+// flight during this 4's logs) -- the slot form's reads, which miss L2
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false,
+          bool kPre = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
@@ -507,8 +519,26 @@ struct ExactObjective {
         step(m, c[m]);
         if (m & 1) __builtin_amdgcn_sched_barrier(0);
       }
+    } else if (kPre) {
+      // groups of 4 elements, the next group's c loads issued before this
+      // group's logs (software pipelined: 8 registers of loads in flight)
+      double nx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nx[j] = cval(u, j, cu);
+#pragma unroll
+      for (int m0 = 0; m0 < kChain; m0 += 4) {
+        double cur[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = nx[j];
+        if (m0 + 4 < kChain) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) nx[j] = cval(u, m0 + 4 + j, cu);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) step(m0 + j, cur[j]);
+      }
     } else {
-#pragma unroll 4
+#pragma unroll NEMO_EXACT_TPUT_UNROLL
       for (int m = 0; m < kChain; ++m) step(m, cval(u, m, cu));
     }
     // the block's 8 accumulators: ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
@@ -682,6 +712,8 @@ struct CArgs {
   const int32_t* plan = nullptr;
   const int32_t* pmeta = nullptr;
   size_t pd = 0;
+  // kSlot (form 7): one plan-ordered c row set per resident wave, [waves][pd]
+  double* sbuf = nullptr;
 };
 
 // The persistent form (option exact_persist): resident blocks whose waves take
@@ -733,14 +765,49 @@ __device__ __forceinline__ void setup_c(Obj& obj, const CArgs& ca, int S, int E,
   __threadfence_block();   // the rows are read back by the same lanes
 }
 
+// The slot form (form 7): the recompute form's c values -- rc_c's operations
+// on the parent's a rows and lv bits, so the same bits -- made once per
+// optimum into this resident wave's own row set `rows` (plan order, one
+// coalesced row per element), which the objective then reads like a stored
+// row set: no division, select or bit test per element and evaluation.  The
+// same lanes write and read the rows.
+template <class Obj, int NS>
+__device__ __forceinline__ void setup_slot(Obj& obj, const CArgs& ca, int S, int b, int k, double s, double lvlo,
+                                           double lvhi, int lane, double* __restrict__ rows) {
+#pragma clang fp contract(off)
+  const double* xa = ca.xa + ((size_t)b * S + k) * ca.pd;
+  const uint32_t* xb = ca.xbits + (size_t)k * NS * kWave;
+  const double rslo = s * (lvlo - 1.0), rshi = s * (lvhi - 1.0);
+  const bool pad_guard = lb::uni(1.0 + rslo == 0.0);
+#pragma unroll
+  for (int u = 0; u < NS; ++u) {
+    const uint32_t bits = xb[(size_t)u * kWave + lane];
+    const int cu = obj.cnt(u), ru = obj.rem(u);
+#pragma unroll 4
+    for (int m = 0; m <= Obj::kChain; ++m) {
+      const size_t at = (size_t)(u * Obj::kRows + m) * kWave + lane;
+      const double a = xa[at];
+      const double sl = ((bits >> m) & 1u) ? rshi : rslo;
+      const double bd = (1.0 - s * a) + sl;
+      const double c = a / bd;
+      const bool real = m < Obj::kChain ? m < cu : ru >= 0;
+      rows[at] = pad_guard ? (real ? c : 0.0) : c;
+    }
+  }
+  obj.cp = rows;
+  __threadfence_block();   // the rows are read back by the same lanes
+}
+
 // one wave per (chain, permissible pair), kExactWaves per block; then the
 // appended blocks of `fin` (eval #1's ll, one lane per chain)
 // kCt (form 4, the cached throughput form): the throughput form's objective
 // loop on the latency form's register c cache, at NEMO_EXACT_CT_WAVES per SIMD
-template <int NS, bool kLat, bool kRc, bool kCt = false, bool kMP = false>
+// kSlot (form 7, the slot form): the throughput form reading c from the
+// resident wave's row set made by setup_slot (persistent launches only)
+template <int NS, bool kLat, bool kRc, bool kCt = false, bool kMP = false, bool kSlot = false>
 __global__ __launch_bounds__(kExactWaves * kWave)
-__attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES,
-                                   kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
+__attribute__((amdgpu_waves_per_eu(kSlot ? NEMO_EXACT_SLOT_WAVES : kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES,
+                                   kSlot ? NEMO_EXACT_SLOT_WAVES : kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_EXACT_TPUT_WAVES))) void local_opt_exact_kernel(
     int S, int E, int npairs, int nchains, const int32_t* __restrict__ pairs, const double* __restrict__ w01,
     const double* __restrict__ anc, const double* __restrict__ ow, const double* __restrict__ xlo,
     const double* __restrict__ xhi, const uint64_t* __restrict__ d1w, int nwords, const int32_t* __restrict__ plan,
@@ -780,7 +847,8 @@ __attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_E
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc && !kSlot, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP,
+                             kSlot && NEMO_EXACT_SLOT_PRE>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
@@ -789,7 +857,11 @@ __attribute__((amdgpu_waves_per_eu(kCt ? NEMO_EXACT_CT_WAVES : kLat ? 2 : NEMO_E
   obj.maxrem = maxrem;
   obj.anc = anc[idx];
   obj.load_plan();
-  setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
+  if constexpr (kSlot)
+    setup_slot<Obj, NS>(obj, ca, S, b, k, s, xlo[k], xhi[k], lane,
+                        ca.sbuf + ((size_t)blockIdx.x * kExactWaves + wv) * ca.pd);
+  else
+    setup_c<Obj, NS, kRc>(obj, ca, S, E, b, k, (size_t)gw, s, xlo[k], xhi[k], owk, d1w, nwords, lane, ~0u);
   obj.nparts = ca.nparts;
   obj.plg = ca.plan;
   obj.pmeta = ca.pmeta;
@@ -1425,6 +1497,8 @@ int lo_resident(int form) {
   if (form == 1) return resident_blocks<local_opt_exact_kernel<NS, true, kRc>>(kExactWaves * kWave);
   if (form == 4) return resident_blocks<local_opt_exact_kernel<NS, false, kRc, true>>(kExactWaves * kWave);
   if (form == 6) return resident_blocks<local_opt_exact_kernel<NS, false, true, false, true>>(kExactWaves * kWave);
+  if (form == 7)
+    return resident_blocks<local_opt_exact_kernel<NS, false, true, false, false, true>>(kExactWaves * kWave);
   return resident_blocks<local_opt_exact_kernel<NS, false, kRc>>(kExactWaves * kWave);
 }
 
@@ -1449,6 +1523,10 @@ void launch_lo(const LoArgs& a, int form, dim3 grid, hipStream_t st) {
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else if (form == 6)   // (internal: the throughput form on two plan parts)
     local_opt_exact_kernel<NS, false, true, false, true><<<grid, kExactWaves * kWave, 0, st>>>(
+        a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
+        a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
+  else if (form == 7)   // (the slot form: recompute rows in, kRc)
+    local_opt_exact_kernel<NS, false, true, false, false, true><<<grid, kExactWaves * kWave, 0, st>>>(
         a.S, a.E, a.npairs, a.nchains, a.pairs, a.w01, a.anc, a.ow, a.xlo, a.xhi, a.d1w, a.nwords, a.plan, a.nh,
         a.maxrem, a.sig0, a.sig1, a.wnew, a.wdag, a.info, a.ca, a.lo_blocks, a.fin);
   else if (form == 4)
@@ -1476,6 +1554,22 @@ void launch_lo_ns(const LoArgs& a, int form, bool rc, dim3 grid, hipStream_t st)
 
 }  // namespace
 
+size_t exact_slot_doubles(const Ctx& c) {
+  int res = 0;
+  switch (c.pw_ns) {
+    case 1: res = lo_resident_ns<1>(7, true); break;
+    case 2: res = lo_resident_ns<2>(7, true); break;
+    case 3: res = lo_resident_ns<3>(7, true); break;
+    case 4: res = lo_resident_ns<4>(7, true); break;
+    case 5: res = lo_resident_ns<5>(7, true); break;
+    case 6: res = lo_resident_ns<6>(7, true); break;
+    case 7: res = lo_resident_ns<7>(7, true); break;
+    case 8: res = lo_resident_ns<8>(7, true); break;
+    default: return 0;
+  }
+  return (size_t)std::max(res, 1) * kExactWaves * exact_plan_doubles(c);
+}
+
 hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t* d_pairs, const double* d_w01,
                                   const double* d_anc, const double* d_ow, double sig0, double sig1, double* d_wnew,
                                   double* d_wdag, int32_t* d_info, const double* d_cs1, double* d_ll1,
@@ -1485,11 +1579,13 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   if (rc ? (size_t)nchains * c.S * exact_plan_doubles(c) > c.cap_xa
          : (size_t)nw * exact_plan_doubles(c) > c.cap_xcbuf)
     return hipErrorInvalidValue;
-  // the latency form while the optima fit in two waves per SIMD (the GPU's
-  // 256 CUs x 4 SIMDs); the throughput form (four per SIMD) beyond; the pair
-  // form for few optima with two slots or more
+  // the latency form up to exact_lat_waves optima (~10 C3 chains), the slot
+  // form (four waves per SIMD, c made once per optimum) beyond -- measured
+  // crossover between 8 and 12 chains, profiles/r6/r6j_forms_ab.txt -- or the
+  // throughput form where the slot form does not apply; the pair form for few
+  // optima with two slots or more
   int form = c.exact_form;
-  if (form == 0) form = nw <= c.exact_lat_waves ? 1 : 2;
+  if (form == 0) form = nw <= c.exact_lat_waves ? 1 : 7;
   // (auto: the pair form up to 3 slots; from 4 its LDS and registers hold it
   // to 1-2 waves per SIMD)
   if (c.pw_ns >= 2 && (c.exact_form == 3 || (c.exact_form == 0 && nw <= c.exact_pair_waves && c.pw_ns <= 3)))
@@ -1500,6 +1596,8 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   if (c.pw_parts > 1) form = 6;
   // the persistent form: at most the resident blocks, the work counter zeroed
   const bool persist = c.exact_persist && c.d_xqueue;
+  // the slot form: one row set per resident wave, so persistent launches only
+  if (form == 7 && !(rc && persist && c.pw_parts == 1 && c.d_xsbuf)) form = 2;
   // the dual form (two optima per wave) needs the register cache's recompute
   // rows, the work queue and at most two slots; else the latency form
   if (form == 5 && !(rc && persist && c.pw_ns <= 2)) form = 1;
@@ -1519,6 +1617,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
       default: return hipErrorInvalidValue;
     }
     lo_blocks = std::min(lo_blocks, std::max(res, 1));
+    if (form == 7 && (size_t)lo_blocks * kExactWaves * exact_plan_doubles(c) > c.cap_xsbuf) return hipErrorInvalidValue;
     const hipError_t me = hipMemsetAsync(c.d_xqueue, 0, sizeof(int), st);
     if (me != hipSuccess) return me;
   }
@@ -1559,6 +1658,7 @@ hipError_t launch_local_opt_exact(Ctx& c, int nchains, int npairs, const int32_t
   a.ca.plan = c.d_pwplan;
   a.ca.pmeta = c.d_pwmeta;
   a.ca.pd = exact_plan_doubles(c);
+  a.ca.sbuf = c.d_xsbuf;
   c.xtrace_n = a.ca.trace ? nw : 0;
   switch (c.pw_ns) {
     case 1: launch_lo_ns<1>(a, form, rc, grid, st); break;

@@ -123,11 +123,11 @@ struct Ctx {
   int exact = 1;
   // the local-optimum kernel's form: 0 auto (the pair form up to
   // exact_pair_waves optima, none by default; the latency form -- its c values
-  // held in registers -- up to exact_lat_waves, 16 C3 chains, measured best
-  // from 1 to 16 chains; the throughput form beyond, best from 32), 1
-  // latency, 2 throughput, 3 pair
+  // held in registers -- up to exact_lat_waves, ~10 C3 chains, measured best
+  // from 1 to 8 chains; the slot form beyond, best from 12), 1 latency, 2
+  // throughput, 3 pair, 4 cached throughput, 5 dual, 7 slot
   int exact_form = 0;
-  int exact_lat_waves = 32768;
+  int exact_lat_waves = 20000;
   int exact_pair_waves = 0;
   bool exact_ok = false;
   double* d_xlo = nullptr;         // [S] numpy's exp(lo_j) (refmath::svml_exp)
@@ -145,6 +145,10 @@ struct Ctx {
   // every evaluation from the parent's plan-ordered a = (lv - 1) ow (d_xa,
   // written by eval #1's order-weight launch) and lv's bit (d_xbits)
   int exact_cform = 1;
+  // the slot form (exact_form 7): one c row set per resident wave of its
+  // kernel, [waves][exact_plan_doubles] (allocated with d_xa, one plan part)
+  double* d_xsbuf = nullptr;
+  size_t cap_xsbuf = 0;
   int exact_xcd = 1;               // option "exact_xcd": XCD-contiguous optimum ranges
   double* d_xa = nullptr;          // [chains][S][exact_plan_doubles]
   size_t cap_xa = 0;               // its size in doubles
@@ -288,6 +292,7 @@ hipError_t launch_local_opt_generic(Ctx& c, int n, const double* d_c, const doub
 // the reference's arithmetic (nemo_exact.hip): supported for this staging?
 bool exact_supported(const Ctx& c);
 size_t exact_plan_doubles(const Ctx& c);   // one plan-ordered row set (per optimum / per parent row)
+size_t exact_slot_doubles(const Ctx& c);   // the slot form's row sets: its resident waves x one row set
 // the local optima recompute c from the parents' a rows (option exact_cform 1,
 // and always for a plan in two parts, which the stored rows do not serve)
 inline bool exact_rc(const Ctx& c) { return c.exact_cform == 1 || c.pw_parts > 1; }

@@ -195,8 +195,8 @@ def test_exact_fused_step_equals_oracle_more_slots(e):
     slots of the wave plan; 3900 and 4097 split into 33 leaves, 5000 into 64;
     from 8193 numpy's np.sum adds buffers of 8192 terms, one wave plan each:
     9000 and 16384 in two, 16392 in three, 40000 in five): one
-    fused step in the throughput
-    and the pair forms, with c stored and recomputed, against the oracle, to
+    fused step in the throughput,
+    pair and slot forms, with c stored and recomputed, against the oracle, to
     the bit (several plans always take the throughput form, c recomputed)."""
     from nemo.nem_order_mcmc import NEMOrderMCMC
     m = generator.synthetic_nem(12, e, 3)
@@ -210,7 +210,7 @@ def test_exact_fused_step_equals_oracle_more_slots(e):
     ora.w = w_raw.copy()
     ref_dag = ora.optimal_weights()
     try:
-        for form in (2, 3):
+        for form in (2, 3, 7):
             for cform in (0, 1):
                 eng.set_option("exact_form", form)
                 eng.set_option("exact_cform", cform)
@@ -345,7 +345,8 @@ def test_exact_score_cells_and_order_weights_together():
 
 def test_exact_kernel_forms_give_the_same_bits():
     """The local-optimum kernel's latency, throughput, pair, cached
-    throughput and dual forms (option exact_form 1 / 2 / 3 / 4 / 5), c stored or recomputed (exact_cform 0 / 1), in
+    throughput, dual and slot forms (option exact_form 1 / 2 / 3 / 4 / 5 / 7), c stored or recomputed (exact_cform 0 /
+    1), in
     launch order or XCD-contiguous order (exact_xcd): the same weights, dag
     weights and lls, to the bit, for one chain and for three."""
     from nemo.nem_order_mcmc import SIG0, SIG1
@@ -358,7 +359,7 @@ def test_exact_kernel_forms_give_the_same_bits():
         anc = np.clip(rng.random((n, 64, 64)) - 0.5, 0, 1)
         outs = []
         try:
-            for form in (1, 2, 3, 4, 5):
+            for form in (1, 2, 3, 4, 5, 7):
                 for cform in (0, 1):
                     for xcd in (0, 1):
                         eng.set_option("exact_form", form)
