@@ -41,10 +41,7 @@
 #define NEMO_EXACT_TPUT_UNROLL 4   // the throughput forms' chain loop unroll
 #endif
 #ifndef NEMO_EXACT_SLOT_WAVES
-#define NEMO_EXACT_SLOT_WAVES 4   // the slot form's waves per SIMD
-#endif
-#ifndef NEMO_EXACT_SLOT_PRE
-#define NEMO_EXACT_SLOT_PRE 0     // the slot form loads a slot's c values at once (ExactObjective::kPre)
+#define NEMO_EXACT_SLOT_WAVES 4   // the slot form's waves per SIMD (3 measured slower, profiles/r6/r6j_forms_ab.txt)
 #endif
 #ifndef NEMO_EXACT_CT_WAVES
 #define NEMO_EXACT_CT_WAVES 3   // the cached throughput form's waves per SIMD (form 4)
@@ -359,10 +356,7 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // the same rounded operations -- so the objective reads 1.1 MB per chain
 // instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
 // starts, counts, remainders, tree partners) is the block's LDS copy.
-// kPre: the chain loop software pipelined (the next 4 elements' c loads in
-// flight during this 4's logs) -- the slot form's reads, which miss L2
-template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false,
-          bool kPre = false>
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
@@ -518,24 +512,6 @@ struct ExactObjective {
       for (int m = 0; m < kChain; ++m) {
         step(m, c[m]);
         if (m & 1) __builtin_amdgcn_sched_barrier(0);
-      }
-    } else if (kPre) {
-      // groups of 4 elements, the next group's c loads issued before this
-      // group's logs (software pipelined: 8 registers of loads in flight)
-      double nx[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nx[j] = cval(u, j, cu);
-#pragma unroll
-      for (int m0 = 0; m0 < kChain; m0 += 4) {
-        double cur[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cur[j] = nx[j];
-        if (m0 + 4 < kChain) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) nx[j] = cval(u, m0 + 4 + j, cu);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) step(m0 + j, cur[j]);
       }
     } else {
 #pragma unroll NEMO_EXACT_TPUT_UNROLL
@@ -847,8 +823,7 @@ __attribute__((amdgpu_waves_per_eu(kSlot ? NEMO_EXACT_SLOT_WAVES : kCt ? NEMO_EX
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc && !kSlot, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP,
-                             kSlot && NEMO_EXACT_SLOT_PRE>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc && !kSlot, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
