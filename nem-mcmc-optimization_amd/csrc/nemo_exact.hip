@@ -40,6 +40,12 @@
 #ifndef NEMO_EXACT_TPUT_UNROLL
 #define NEMO_EXACT_TPUT_UNROLL 4   // the throughput forms' chain loop unroll
 #endif
+#ifndef NEMO_EXACT_SLOT_PAIRS
+#define NEMO_EXACT_SLOT_PAIRS 1   // the slot form's row set in element pairs (ExactObjective::kPairs)
+#endif
+#ifndef NEMO_EXACT_SLOT_GROUP
+#define NEMO_EXACT_SLOT_GROUP 4   // the slot form's pair loads in flight together (2, 4 or 8)
+#endif
 #ifndef NEMO_EXACT_SLOT_WAVES
 #define NEMO_EXACT_SLOT_WAVES 4   // the slot form's waves per SIMD (3 measured slower, profiles/r6/r6j_forms_ab.txt)
 #endif
@@ -356,10 +362,15 @@ __global__ __launch_bounds__(256) void exact_seq_sum_kernel(int E, int batch, co
 // the same rounded operations -- so the objective reads 1.1 MB per chain
 // instead of one 17 KB row set per optimum.  The plan itself (per lane: chain
 // starts, counts, remainders, tree partners) is the block's LDS copy.
-template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false>
+// kPairs (the slot form): the row set's 16 chain rows stored as 8 rows of
+// element pairs (lane l's elements 2p and 2p + 1 side by side), so one 16-byte
+// load brings two c values; the remainder row as before
+template <int NS, bool kPlan, bool kLat, bool kPair = false, bool kRc = false, bool kCache = false, bool kMP = false,
+          bool kPairs = false>
 struct ExactObjective {
   static constexpr int kChain = 16;  // a leaf block of <= 128 elements: <= 16 per chain
   static constexpr int kRows = kChain + 1;
+  static constexpr bool kPairsLayout = kPairs;
   const double* cp;
   // kCache (the latency form's recompute rows, 2 waves per SIMD): the lane's
   // c values made once per optimum (fill_cache) and held in registers through
@@ -439,6 +450,7 @@ struct ExactObjective {
     return m < cu ? cp[start(u) + 8 * m] : 0.0;
   }
   __device__ __forceinline__ double crem(int u, int ru) const {
+    if (kPairs) return cp[(u * kRows + kChain) * kWave + lane];
     if (kCache) return cc[kCache ? u : 0][kCache ? kChain : 0];
     if (kRc) return rc_c(u, kChain, ru >= 0);
     if (kPlan) return cp[(u * kRows + kChain) * kWave + lane];
@@ -504,7 +516,24 @@ struct ExactObjective {
     // (the cached throughput form keeps the unroll by 4: its cache then lives
     // in scratch, which measured faster than registers at its 3-wave budget --
     // 1.61 against 1.84 ms per 16-chain step, profiles/r6/r6f_forms_sweep.txt)
-    if (kLat) {
+    if (kPairs) {
+      // a group's pairs all requested before the first one's logs (the
+      // scheduling barrier keeps the later loads from sinking to their use)
+      constexpr int kG = NEMO_EXACT_SLOT_GROUP;
+      const double2* pr = reinterpret_cast<const double2*>(cp + (size_t)u * kRows * kWave) + lane;
+#pragma unroll 1
+      for (int p = 0; p < kChain / 2; p += kG) {
+        double2 cg[kG];
+#pragma unroll
+        for (int g = 0; g < kG; ++g) cg[g] = pr[(p + g) * kWave];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+          step(2 * (p + g), cg[g].x);
+          step(2 * (p + g) + 1, cg[g].y);
+        }
+      }
+    } else if (kLat) {
       double c[kChain];
 #pragma unroll
       for (int m = 0; m < kChain; ++m) c[m] = cval(u, m, cu);
@@ -762,12 +791,16 @@ __device__ __forceinline__ void setup_slot(Obj& obj, const CArgs& ca, int S, int
 #pragma unroll 4
     for (int m = 0; m <= Obj::kChain; ++m) {
       const size_t at = (size_t)(u * Obj::kRows + m) * kWave + lane;
+      // (kPairs: chain rows as pairs, element m of pair m / 2 at its m % 2)
+      const size_t to = Obj::kPairsLayout && m < Obj::kChain
+                            ? (size_t)u * Obj::kRows * kWave + ((size_t)(m >> 1) * kWave + lane) * 2 + (m & 1)
+                            : at;
       const double a = xa[at];
       const double sl = ((bits >> m) & 1u) ? rshi : rslo;
       const double bd = (1.0 - s * a) + sl;
       const double c = a / bd;
       const bool real = m < Obj::kChain ? m < cu : ru >= 0;
-      rows[at] = pad_guard ? (real ? c : 0.0) : c;
+      rows[to] = pad_guard ? (real ? c : 0.0) : c;
     }
   }
   obj.cp = rows;
@@ -823,7 +856,8 @@ __attribute__((amdgpu_waves_per_eu(kSlot ? NEMO_EXACT_SLOT_WAVES : kCt ? NEMO_EX
   const double s = w01[idx];
   const double* owk = ow + ((size_t)b * (S + 1) + k) * E;
   const long long t_start = ca.trace ? (long long)wall_clock64() : 0;
-  using Obj = ExactObjective<NS, true, kLat, false, kRc && !kSlot, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP>;
+  using Obj = ExactObjective<NS, true, kLat, false, kRc && !kSlot, (kLat || kCt) && kRc && NEMO_EXACT_CCACHE, kMP,
+                             kSlot && NEMO_EXACT_SLOT_PAIRS>;
   Obj obj;
   obj.tb = tabs.view();
   obj.pl = pl;
